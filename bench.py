@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the RTIOW cover-scene render on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32]
+  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend)
+
+Workload (BASELINE.json configs[1]): cover scene (generateRandomScene,
+DefaultPrng.init(42), main.zig:157-221), 1200x675 (16:9), 500 spp per GPU,
+depth 50, scene resident in HBM before the timed region.  A step is one whole
+frame: the trace megakernel + the chunk-combine/quantise kernel (+ at N > 1
+the RCCL gather of every rank's interleaved rows to rank 0).
+
+Weak scaling: at N GPUs the job is the same 1200x675 frame at N*500 spp,
+image rows interleaved across ranks (rank r: rows r, r+N, ...), so every rank
+traces 1200 x 675/N x 500N ~= 405 M samples, bit-identical to the same rows of
+a 1-GPU render of the N*500-spp frame.  value = samples of all ranks / max
+rank time.
+
+Extra fields: roofline (dominant kernel = trace; HIP events on the render
+stream), cpu_baseline (oracle Tier A = the reference's algorithm, sequential
+RNG, one core, on a bounded sample of the same frame).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracinginoneweekend.zig_amd"))
+
+W_IMG, ASPECT, SPP, DEPTH, SEED = 1200, 16 / 9, 500, 50, 42
+# Algorithmic flops per sphere test, counted from hittable.zig:96-101 with the
+# per-segment invariants hoisted: static 17, moving 23.
+FLOP_STATIC, FLOP_MOVING = 17, 23
+PEAK_FP64_VALU_TF = 78.6   # MI355X FP64 vector (MI355X_MICROARCH.md: FP32 157.3 = 2x)
+PEAK_FP32_VALU_TF = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--spp", type=int, default=SPP, help="spp per GPU (default 500 = configs[1])")
+    ap.add_argument("--width", type=int, default=W_IMG)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-f32-variant", action="store_true")
+    ap.add_argument("--cpu-spp", type=int, default=16, help="spp of the bounded CPU sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(width, height, spp_sample):
+    """Oracle Tier A (the reference's render loop restated: f64, one sequential
+    DefaultPrng(42) stream, recursive rayColor) on one core, on the same frame
+    at reduced spp.  Test infrastructure used only as the timed CPU baseline."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import rtw_oracle as O
+    O.lib()
+    sc, rng = O.cover_scene(SEED)
+    cam = O.cover_camera(ASPECT)
+    t0 = time.perf_counter()
+    _, _, st = O.render_tier_a(sc, cam, rng, width, height, spp_sample, DEPTH)
+    dt = time.perf_counter() - t0
+    try:
+        cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        cpu = "unknown"
+    return {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
+                      f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import rtw_amd as R
+    from rtw_amd.device import TorchRenderer
+    from rtw_amd.shard import gather_image, shard_rows
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (no CPU fallback)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W = args.width
+    H = R.image_height(W, ASPECT)
+    spp = args.spp * world  # weak scaling: the frame gets N x spp
+    sph, mats, _ = R.cover_scene(SEED)
+    cam = R.cover_camera(ASPECT)
+    rb, rs, rc = shard_rows(H, rank, world)
+    params = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
+                           precision=args.precision)
+    rend = TorchRenderer(sph, mats, local)
+    out = torch.empty((rc, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
+    samples_rank = rc * W * spp
+
+    # Untimed: counts pass (algorithmic flops of one trace launch) + warmup.
+    counts = rend.counts(cam, params)
+    for _ in range(args.warmup):
+        rend.render(cam, params, out=out)
+        if world > 1:
+            gather_image(out, H, rank, world)
+    torch.cuda.synchronize()
+
+    # One HIP-event pair per step brackets that step's trace-kernel launch on
+    # the render stream (torch's current stream), read after the region.
+    timers = [R.Timer() for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        rend.render(cam, params, out=out, timer=timers[i])
+        if world > 1:
+            gather_image(out, H, rank, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    per = [t.elapsed_ms() for t in timers]
+    trace_ms_avg = sum(per) / len(per)
+    for t in timers:
+        t.close()
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([samples_rank], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tot)
+        samples_all = float(tot.item())
+    else:
+        samples_all = float(samples_rank)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = samples_all * args.steps / elapsed / 1e6
+
+    # Roofline of the dominant kernel (trace): algorithmic flops per launch /
+    # average launch time.  HBM: algorithmic bytes per launch = one f64x3
+    # chunk sum (24 B) per (pixel, chunk) unit written + scene tables read.
+    flops = counts["static_tests"] * FLOP_STATIC + counts["moving_tests"] * FLOP_MOVING
+    achieved_tf = flops / (trace_ms_avg * 1e-3) / 1e12
+    peak = PEAK_FP64_VALU_TF if args.precision == "f64" else PEAK_FP32_VALU_TF
+    chunk = min(R.DEFAULT_CHUNK, spp)
+    n_chunks = (spp + chunk - 1) // chunk
+    hbm_bytes = rc * W * n_chunks * 24
+    hbm_gbs = hbm_bytes / (trace_ms_avg * 1e-3) / 1e9
+    roofline = {
+        "bound": "valu-fp64" if args.precision == "f64" else "valu-fp32",
+        "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
+        "frac": round(achieved_tf / peak, 4),
+        "traffic": None,
+        "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
+        "flop_per_launch": flops, "segments_per_launch": counts["segments"],
+        "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
+        "note": "megakernel is FP64-VALU + divergence bound; MFMA n/a (no contraction); HBM traffic is "
+                "~24 B per 32 samples by construction (DESIGN.md §Roofline)",
+    }
+
+    extra = {}
+    if not args.no_f32_variant and args.precision == "f64":
+        p32 = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc, precision="f32")
+        for _ in range(max(1, args.warmup)):
+            rend.render(cam, p32, out=out)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        a = time.perf_counter()
+        for _ in range(args.steps):
+            rend.render(cam, p32, out=out)
+            if world > 1:
+                gather_image(out, H, rank, world)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e32 = time.perf_counter() - a
+        if world > 1:
+            t = torch.tensor([e32], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e32 = float(t.item())
+        extra["f32_hybrid_variant"] = {"value": round(samples_all * args.steps / e32 / 1e6, 2),
+                                       "ms_per_step": round(e32 / args.steps * 1e3, 3),
+                                       "note": "precision=f32 (f32 + f64 wide spheres + convex self-skip); "
+                                               "not the headline: the reference computes in f64"}
+
+    res = {
+        "metric": "Msamples/sec (pixels x spp / s), RTIOW cover scene; trace-kernel roofline",
+        "value": round(value, 2),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic: the reference's own scene generator (seed 42); no external data",
+        "config": {"workload": f"RTIOW cover scene {W}x{H}, {args.spp} spp per GPU ({spp} spp frame), depth {DEPTH}, "
+                               f"rows interleaved over {world} GPU(s)",
+                   "width": W, "height": H, "spp_frame": spp, "max_depth": DEPTH, "seed": SEED,
+                   "precision": args.precision, "parallelism": f"rows{world}"},
+        "roofline": roofline,
+    }
+    res.update(extra)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(W, H, args.cpu_spp)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,238 @@
+"""ctypes front-end of the CPU ORACLE (oracle/librtw_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — as the checker or the timed CPU baseline, never
+as the product path.  See rtw_oracle.h for the Tier A / Tier B definitions and
+the parity status ("parity unpinned" against the Zig binary; pinned by RNG
+KATs and the independent Python restatement in rtw_oracle_py.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtw_oracle.so")
+
+MAX_SPHERES = 1024
+LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC = 0, 1, 2, 3
+
+
+class Sphere(C.Structure):
+    _fields_ = [("c0", C.c_double * 3), ("c1", C.c_double * 3), ("radius", C.c_double),
+                ("t0", C.c_double), ("t1", C.c_double), ("moving", C.c_uint32), ("mat", C.c_uint32)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("albedo", C.c_double * 3), ("albedo_odd", C.c_double * 3),
+                ("fuzz", C.c_double), ("ir", C.c_double)]
+
+
+class Scene(C.Structure):
+    _fields_ = [("n_spheres", C.c_uint32), ("n_mats", C.c_uint32),
+                ("spheres", Sphere * MAX_SPHERES), ("mats", Material * MAX_SPHERES)]
+
+
+class Camera(C.Structure):
+    _fields_ = [(n, C.c_double * 3) for n in
+                ("origin", "horizontal", "vertical", "lower_left_corner", "u", "v", "w")] + \
+               [("lens_radius", C.c_double), ("time0", C.c_double), ("time1", C.c_double)]
+
+
+class Params(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32),
+                ("max_depth", C.c_uint32), ("seed", C.c_uint64), ("background", C.c_double * 3),
+                ("row_begin", C.c_uint32), ("row_stride", C.c_uint32), ("row_count", C.c_uint32),
+                ("chunk", C.c_uint32), ("precision", C.c_uint32), ("threads", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("static_tests", C.c_uint64),
+                ("moving_tests", C.c_uint64), ("draws", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+U64x4 = C.c_uint64 * 4
+_lib = None
+
+
+def build():
+    """Compile the oracle with its own Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.ro_splitmix64_next.restype = C.c_uint64
+        L.ro_splitmix64_next.argtypes = [C.POINTER(C.c_uint64)]
+        L.ro_xoshiro256_seed.argtypes = [U64x4, C.c_uint64]
+        L.ro_xoshiro256_next.restype = C.c_uint64
+        L.ro_xoshiro256_next.argtypes = [U64x4]
+        L.ro_random_f64.restype = C.c_double
+        L.ro_random_f64.argtypes = [U64x4]
+        L.ro_random_f32.restype = C.c_float
+        L.ro_random_f32.argtypes = [U64x4]
+        L.ro_zig_pow.restype = C.c_double
+        L.ro_zig_pow.argtypes = [C.c_double, C.c_double]
+        L.ro_camera_init.argtypes = [C.POINTER(Camera)] + [C.c_double * 3] * 3 + [C.c_double] * 6
+        L.ro_cover_scene.restype = C.c_int
+        L.ro_cover_scene.argtypes = [U64x4, C.POINTER(Scene)]
+        L.ro_image_height.restype = C.c_uint32
+        L.ro_image_height.argtypes = [C.c_uint32, C.c_double]
+        L.ro_render_tier_a.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3,
+                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, U64x4,
+                                       C.c_void_p, C.c_void_p, C.POINTER(Stats)]
+        L.ro_main_cover.argtypes = [C.c_uint32, C.c_double, C.c_uint32, C.c_uint32, C.c_uint64,
+                                    C.c_void_p, C.POINTER(Stats)]
+        L.ro_render_tier_b.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+                                       C.c_void_p, C.c_void_p, C.POINTER(Stats)]
+        L.ro_quantize.restype = C.c_uint8
+        L.ro_quantize.argtypes = [C.c_double, C.c_double]
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------- RNG ----
+class ZigRandom:
+    """DefaultPrng (Xoshiro256++) stream, as main.zig:300 uses it."""
+
+    def __init__(self, seed: int | None = None, state=None):
+        self.s = U64x4()
+        if state is not None:
+            for i in range(4):
+                self.s[i] = state[i]
+        else:
+            lib().ro_xoshiro256_seed(self.s, seed)
+
+    def next(self) -> int:
+        return lib().ro_xoshiro256_next(self.s)
+
+    def f64(self) -> float:
+        return lib().ro_random_f64(self.s)
+
+    def f32(self) -> float:
+        return lib().ro_random_f32(self.s)
+
+    def state(self):
+        return [int(self.s[i]) for i in range(4)]
+
+
+def splitmix64_seq(seed: int, n: int):
+    st = C.c_uint64(seed)
+    return [lib().ro_splitmix64_next(C.byref(st)) for _ in range(n)]
+
+
+# -------------------------------------------------------------- scene ----
+COVER_BG = (0.70, 0.80, 1.00)
+
+
+def image_height(width: int, aspect: float) -> int:
+    return int(lib().ro_image_height(width, aspect))
+
+
+def cover_scene(seed: int = 42):
+    """generateRandomScene on a fresh DefaultPrng.init(seed); returns
+    (Scene, ZigRandom positioned after the build)."""
+    rng = ZigRandom(seed)
+    sc = Scene()
+    lib().ro_cover_scene(rng.s, C.byref(sc))
+    return sc, rng
+
+
+def cover_camera(aspect: float) -> Camera:
+    """Scene-1 camera (main.zig:320-326, :366-376)."""
+    cam = Camera()
+    arr = C.c_double * 3
+    lib().ro_camera_init(C.byref(cam), arr(13, 2, 3), arr(0, 0, 0), arr(0, 1, 0),
+                         20.0, aspect, 0.1, 10.0, 0.0, 1.0)
+    return cam
+
+
+def scene_table(sc: Scene) -> dict:
+    """Plain-python dump of the flattened scene (for golden fixtures)."""
+    sph = []
+    for i in range(sc.n_spheres):
+        s = sc.spheres[i]
+        sph.append({"c0": list(s.c0), "c1": list(s.c1), "radius": s.radius, "t0": s.t0, "t1": s.t1,
+                    "moving": int(s.moving), "mat": int(s.mat)})
+    mats = []
+    for i in range(sc.n_mats):
+        m = sc.mats[i]
+        mats.append({"kind": int(m.kind), "albedo": list(m.albedo), "albedo_odd": list(m.albedo_odd),
+                     "fuzz": m.fuzz, "ir": m.ir})
+    return {"spheres": sph, "materials": mats}
+
+
+def scene_from_table(t: dict) -> Scene:
+    sc = Scene()
+    sc.n_spheres = len(t["spheres"])
+    sc.n_mats = len(t["materials"])
+    for i, s in enumerate(t["spheres"]):
+        d = sc.spheres[i]
+        d.c0[:] = s["c0"]
+        d.c1[:] = s["c1"]
+        d.radius, d.t0, d.t1 = s["radius"], s["t0"], s["t1"]
+        d.moving, d.mat = s["moving"], s["mat"]
+    for i, m in enumerate(t["materials"]):
+        d = sc.mats[i]
+        d.kind = m["kind"]
+        d.albedo[:] = m["albedo"]
+        d.albedo_odd[:] = m["albedo_odd"]
+        d.fuzz, d.ir = m["fuzz"], m["ir"]
+    return sc
+
+
+# ------------------------------------------------------------- render ----
+def main_cover(width: int, aspect: float, spp: int, depth: int = 50, seed: int = 42):
+    """Tier A: the whole reference main() for scene 1 -> (H, W, 3) uint8."""
+    H = image_height(width, aspect)
+    out = np.zeros((H, width, 3), np.uint8)
+    st = Stats()
+    lib().ro_main_cover(width, aspect, spp, depth, seed, out.ctypes.data, C.byref(st))
+    return out, st.as_dict()
+
+
+def render_tier_a(scene: Scene, cam: Camera, rng: ZigRandom, width: int, height: int, spp: int,
+                  depth: int = 50, bg=COVER_BG, want_sum=False):
+    out = np.zeros((height, width, 3), np.uint8)
+    sums = np.zeros((height, width, 3), np.float64) if want_sum else None
+    st = Stats()
+    lib().ro_render_tier_a(C.byref(scene), C.byref(cam), (C.c_double * 3)(*bg), width, height, spp,
+                           depth, rng.s, out.ctypes.data, sums.ctypes.data if want_sum else None,
+                           C.byref(st))
+    return out, sums, st.as_dict()
+
+
+def render_tier_b(scene: Scene, cam: Camera, width: int, height: int, spp: int, depth: int = 50,
+                  seed: int = 42, bg=COVER_BG, row_begin: int = 0, row_stride: int = 1,
+                  row_count: int | None = None, chunk: int = 0, precision: int = 0,
+                  threads: int = 0, want_mean=False):
+    """Tier B (the GPU contract) -> (rows, W, 3) uint8 [, mean f32]."""
+    if row_count is None:
+        row_count = (height - row_begin + row_stride - 1) // row_stride
+    p = Params(width, height, spp, depth, seed, (C.c_double * 3)(*bg), row_begin, row_stride,
+               row_count, chunk, precision, threads)
+    out = np.zeros((row_count, width, 3), np.uint8)
+    mean = np.zeros((row_count, width, 3), np.float32) if want_mean else None
+    st = Stats()
+    lib().ro_render_tier_b(C.byref(scene), C.byref(cam), C.byref(p), out.ctypes.data,
+                           mean.ctypes.data if want_mean else None, C.byref(st))
+    if want_mean:
+        return out, mean, st.as_dict()
+    return out, st.as_dict()
+
+
+def write_ppm(path: str, img: np.ndarray):
+    h, w, _ = img.shape
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h))
+        f.write(np.ascontiguousarray(img, np.uint8).tobytes())

@@ -1,0 +1,486 @@
+// rtw_capi.hip — the C ABI (include/rtw_hip.h): validation, scene upload,
+// workspace sizing, kernel launches.  Replaces the render loop of
+// src/main.zig:378-402.  No exception and no C++ type crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "rtw_hip.h"
+#include "rtw_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int status, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return status;
+}
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(RTW_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+uint64_t splitmix_first(uint64_t seed) {  // SplitMix64.init(seed).next()
+  uint64_t z = seed + 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+struct DevInfo {
+  int cus = 0;
+  int bpc[2] = {0, 0};  // blocks per CU per precision (at the LDS size used)
+  size_t bpc_lds[2] = {(size_t)-1, (size_t)-1};
+};
+std::mutex g_dev_mu;
+std::map<int, DevInfo> g_dev;
+
+int device_cus(int dev) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto& d = g_dev[dev];
+  if (d.cus == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    d.cus = v;
+  }
+  return d.cus;
+}
+int blocks_per_cu(int dev, int prec, size_t lds) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto& d = g_dev[dev];
+  if (d.bpc_lds[prec] != lds) {
+    d.bpc[prec] = rtwk::trace_blocks_per_cu(prec, lds);
+    d.bpc_lds[prec] = lds;
+  }
+  return d.bpc[prec];
+}
+
+}  // namespace
+
+struct rtw_scene_s {
+  int device = 0;
+  uint32_t n = 0, nm = 0, ng = 0;
+  uint32_t n_static = 0, n_moving = 0, n_wide = 0;
+  void* buf = nullptr;  // one allocation holding every table
+  rtwk::SceneView<double> v64{};
+  rtwk::SceneView<float> v32{};
+};
+
+struct rtw_timer_s {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool recorded = false;
+};
+
+extern "C" {
+
+int rtw_abi_version(void) { return RTW_ABI_VERSION; }
+
+const char* rtw_last_error(void) { return g_err.c_str(); }
+
+int rtw_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* mats, uint32_t nm,
+                     rtw_scene* out) {
+  if (!out) return fail(RTW_EINVAL, "rtw_scene_create: out is NULL");
+  *out = nullptr;
+  if (n > 0 && !spheres) return fail(RTW_EINVAL, "rtw_scene_create: spheres is NULL");
+  if (nm > 0 && !mats) return fail(RTW_EINVAL, "rtw_scene_create: materials is NULL");
+  if (n > RTW_MAX_SPHERES || nm > RTW_MAX_SPHERES)
+    return fail(RTW_UNSUPPORTED, "rtw_scene_create: %u spheres / %u materials exceeds %u (BVH path not built)",
+                n, nm, RTW_MAX_SPHERES);
+  for (uint32_t i = 0; i < nm; ++i) {
+    if (mats[i].kind > RTW_DIELECTRIC)
+      return fail(RTW_UNSUPPORTED, "material %u: kind %u not supported on the GPU path", i, mats[i].kind);
+  }
+  // Distinct (t0, t1) pairs of moving spheres -> time groups.
+  std::vector<std::pair<double, double>> groups;
+  std::vector<uint32_t> meta(n);
+  uint32_t n_moving = 0, n_wide = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const rtw_sphere& s = spheres[i];
+    if (s.mat >= nm) return fail(RTW_EINVAL, "sphere %u: material index %u >= %u", i, s.mat, nm);
+    if (s.moving > 1) return fail(RTW_EINVAL, "sphere %u: moving flag %u", i, s.moving);
+    uint32_t m = s.mat << 8;
+    if (s.moving) {
+      ++n_moving;
+      uint32_t g = 0;
+      while (g < groups.size() && !(groups[g].first == s.t0 && groups[g].second == s.t1)) ++g;
+      if (g == groups.size()) {
+        if (groups.size() >= rtwk::kMaxTimeGroups)
+          return fail(RTW_UNSUPPORTED, "more than %u distinct moving-sphere time ranges", rtwk::kMaxTimeGroups);
+        groups.emplace_back(s.t0, s.t1);
+      }
+      m |= rtwk::kMoving | (g << 2);
+    }
+    if (s.radius >= rtwk::kWideRadius) {
+      m |= rtwk::kWide;
+      ++n_wide;
+    }
+    meta[i] = m;
+  }
+  const uint32_t ng = (uint32_t)groups.size();
+  // Host tables.
+  std::vector<double> sph64((size_t)8 * n), mat64((size_t)8 * nm), tg64((size_t)2 * ng);
+  std::vector<float> sph32((size_t)8 * n), mat32((size_t)8 * nm), tg32((size_t)2 * ng);
+  std::vector<uint32_t> kind(nm);
+  for (uint32_t i = 0; i < n; ++i) {
+    const rtw_sphere& s = spheres[i];
+    const double rec[8] = {s.c0[0], s.c0[1], s.c0[2], s.c1[0] - s.c0[0], s.c1[1] - s.c0[1], s.c1[2] - s.c0[2],
+                           s.radius * s.radius, s.radius};
+    for (int k = 0; k < 8; ++k) sph64[8 * i + k] = rec[k];
+    for (int k = 0; k < 6; ++k) sph32[8 * i + k] = (float)rec[k];
+    const float rf = (float)s.radius;
+    sph32[8 * i + 6] = rf * rf;  // f32 mode: r*r in f32 (tierb_core.h prep)
+    sph32[8 * i + 7] = rf;
+  }
+  for (uint32_t i = 0; i < nm; ++i) {
+    const rtw_material& m = mats[i];
+    const double rec[8] = {m.albedo[0], m.albedo[1], m.albedo[2], m.albedo_odd[0], m.albedo_odd[1],
+                           m.albedo_odd[2], m.fuzz, m.ir};
+    for (int k = 0; k < 8; ++k) {
+      mat64[8 * i + k] = rec[k];
+      mat32[8 * i + k] = (float)rec[k];
+    }
+    kind[i] = m.kind;
+  }
+  for (uint32_t g = 0; g < ng; ++g) {
+    tg64[2 * g] = groups[g].first;
+    tg64[2 * g + 1] = groups[g].second;
+    tg32[2 * g] = (float)groups[g].first;
+    tg32[2 * g + 1] = (float)groups[g].second;
+  }
+  // One device allocation, 256-B aligned sub-buffers.
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t o_sph64 = 0, s_sph64 = al(sph64.size() * 8 + 8);
+  const size_t o_mat64 = o_sph64 + s_sph64, s_mat64 = al(mat64.size() * 8 + 8);
+  const size_t o_tg64 = o_mat64 + s_mat64, s_tg64 = al(tg64.size() * 8 + 8);
+  const size_t o_sph32 = o_tg64 + s_tg64, s_sph32 = al(sph32.size() * 4 + 4);
+  const size_t o_mat32 = o_sph32 + s_sph32, s_mat32 = al(mat32.size() * 4 + 4);
+  const size_t o_tg32 = o_mat32 + s_mat32, s_tg32 = al(tg32.size() * 4 + 4);
+  const size_t o_meta = o_tg32 + s_tg32, s_meta = al(meta.size() * 4 + 4);
+  const size_t o_kind = o_meta + s_meta, s_kind = al(kind.size() * 4 + 4);
+  const size_t total = o_kind + s_kind;
+  std::vector<unsigned char> host(total, 0);
+  auto cp = [&](size_t off, const void* p, size_t bytes) {
+    if (bytes) std::memcpy(host.data() + off, p, bytes);
+  };
+  cp(o_sph64, sph64.data(), sph64.size() * 8);
+  cp(o_mat64, mat64.data(), mat64.size() * 8);
+  cp(o_tg64, tg64.data(), tg64.size() * 8);
+  cp(o_sph32, sph32.data(), sph32.size() * 4);
+  cp(o_mat32, mat32.data(), mat32.size() * 4);
+  cp(o_tg32, tg32.data(), tg32.size() * 4);
+  cp(o_meta, meta.data(), meta.size() * 4);
+  cp(o_kind, kind.data(), kind.size() * 4);
+
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  void* d = nullptr;
+  if (hipMalloc(&d, total) != hipSuccess) return fail(RTW_ENOMEM, "rtw_scene_create: hipMalloc(%zu)", total);
+  if (hipMemcpy(d, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(RTW_EHIP, "rtw_scene_create: hipMemcpy failed");
+  }
+  auto* sc = new rtw_scene_s;
+  sc->device = dev;
+  sc->n = n;
+  sc->nm = nm;
+  sc->ng = ng;
+  sc->n_moving = n_moving;
+  sc->n_static = n - n_moving;
+  sc->n_wide = n_wide;
+  sc->buf = d;
+  auto* b = static_cast<unsigned char*>(d);
+  sc->v64 = {reinterpret_cast<const double*>(b + o_sph64), reinterpret_cast<const uint32_t*>(b + o_meta),
+             reinterpret_cast<const double*>(b + o_mat64), reinterpret_cast<const uint32_t*>(b + o_kind),
+             reinterpret_cast<const double*>(b + o_tg64),  reinterpret_cast<const double*>(b + o_sph64),
+             reinterpret_cast<const double*>(b + o_tg64),  n, nm, ng, 0};
+  sc->v32 = {reinterpret_cast<const float*>(b + o_sph32), reinterpret_cast<const uint32_t*>(b + o_meta),
+             reinterpret_cast<const float*>(b + o_mat32), reinterpret_cast<const uint32_t*>(b + o_kind),
+             reinterpret_cast<const float*>(b + o_tg32),  reinterpret_cast<const double*>(b + o_sph64),
+             reinterpret_cast<const double*>(b + o_tg64), n, nm, ng, 0};
+  *out = sc;
+  return RTW_OK;
+}
+
+int rtw_scene_destroy(rtw_scene sc) {
+  if (!sc) return RTW_OK;
+  if (sc->buf) (void)hipFree(sc->buf);
+  delete sc;
+  return RTW_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+uint32_t eff_chunk(const rtw_params* p) {
+  const uint32_t c = p->chunk ? p->chunk : RTW_DEFAULT_CHUNK;
+  return std::min(c, p->spp);
+}
+uint32_t n_chunks(const rtw_params* p) {
+  const uint32_t c = eff_chunk(p);
+  return (p->spp + c - 1) / c;
+}
+
+int validate(const rtw_params* p) {
+  if (!p) return fail(RTW_EINVAL, "params is NULL");
+  if (p->width < 2 || p->height < 2)
+    return fail(RTW_EINVAL, "image %ux%u: width and height must be >= 2 (main.zig:390-391 divide by W-1, H-1)",
+                p->width, p->height);
+  if (p->spp == 0) return fail(RTW_EINVAL, "spp must be >= 1");
+  if ((uint64_t)p->width * p->height > (1ull << 24))
+    return fail(RTW_UNSUPPORTED, "image of %llu pixels exceeds 2^24 (per-sample RNG key layout)",
+                (unsigned long long)p->width * p->height);
+  if (p->spp > (1u << 24)) return fail(RTW_UNSUPPORTED, "spp %u exceeds 2^24", p->spp);
+  if (p->row_stride == 0 || p->row_count == 0) return fail(RTW_EINVAL, "row_stride and row_count must be >= 1");
+  if ((uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->height)
+    return fail(RTW_EINVAL, "rows %u + k*%u (k < %u) exceed height %u", p->row_begin, p->row_stride,
+                p->row_count, p->height);
+  if (p->precision > RTW_PRECISION_F32) return fail(RTW_EINVAL, "precision %u", p->precision);
+  const uint64_t tiles = (uint64_t)((p->width + rtwk::kTileW - 1) / rtwk::kTileW) *
+                         ((p->row_count + rtwk::kTileH - 1) / rtwk::kTileH);
+  const uint64_t units = tiles * 64ull * n_chunks(p);
+  if (units > 0x7FFFFFFFull)  // headroom: waves overshoot the queue by < 2^31 units
+    return fail(RTW_UNSUPPORTED, "%llu work units exceed the 32-bit queue; raise params.chunk",
+                (unsigned long long)units);
+  return RTW_OK;
+}
+
+struct WsLayout {
+  size_t partial_off, partial_bytes, counter_off, stats_off, total;
+};
+WsLayout ws_layout(const rtw_params* p) {
+  WsLayout w;
+  w.partial_off = 0;
+  w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
+  w.counter_off = (w.partial_bytes + 255) & ~(size_t)255;
+  w.stats_off = w.counter_off + 256;
+  w.total = w.stats_off + 256;
+  return w;
+}
+
+template <typename R>
+void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_camera* cam, const rtw_params* p,
+               unsigned char* ws, const WsLayout& L) {
+  std::memset(&a, 0, sizeof(a));
+  a.sc = v;
+  for (int k = 0; k < 3; ++k) {
+    a.origin[k] = (R)cam->origin[k];
+    a.horizontal[k] = (R)cam->horizontal[k];
+    a.vertical[k] = (R)cam->vertical[k];
+    a.llc[k] = (R)cam->lower_left_corner[k];
+    a.cu[k] = (R)cam->u[k];
+    a.cv[k] = (R)cam->v[k];
+    a.bg[k] = (R)p->background[k];
+  }
+  a.lens_radius = (R)cam->lens_radius;
+  a.time0 = (R)cam->time0;
+  a.time1 = (R)cam->time1;
+  a.tmin = (R)0.001;
+  a.W = p->width;
+  a.H = p->height;
+  a.spp = p->spp;
+  a.max_depth = p->max_depth;
+  a.chunk = eff_chunk(p);
+  a.n_chunks = n_chunks(p);
+  a.row_begin = p->row_begin;
+  a.row_stride = p->row_stride;
+  a.row_count = p->row_count;
+  a.tiles_x = (p->width + rtwk::kTileW - 1) / rtwk::kTileW;
+  const uint32_t tiles_y = (p->row_count + rtwk::kTileH - 1) / rtwk::kTileH;
+  a.total_units = a.tiles_x * tiles_y * 64u * a.n_chunks;
+  a.seed_base = splitmix_first(p->seed);
+  a.partial = reinterpret_cast<double*>(ws + L.partial_off);
+  a.counter = reinterpret_cast<uint32_t*>(ws + L.counter_off);
+  a.stats = reinterpret_cast<unsigned long long*>(ws + L.stats_off);
+}
+
+size_t lds_bytes(const rtw_scene_s* sc, int prec) {
+  const size_t r = prec == 1 ? 4 : 8;
+  return r * (8 * (size_t)sc->n + 8 * (size_t)sc->nm + 2 * (size_t)sc->ng) + 4 * ((size_t)sc->n + sc->nm) + 16;
+}
+
+int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace, size_t ws_bytes,
+               uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, bool stats) {
+  const WsLayout L = ws_layout(p);
+  if (!workspace || ws_bytes < L.total)
+    return fail(RTW_EINVAL, "workspace %zu bytes < required %zu", ws_bytes, L.total);
+  if ((reinterpret_cast<uintptr_t>(workspace) & 255) != 0) return fail(RTW_EINVAL, "workspace not 256-B aligned");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != sc->device)
+    return fail(RTW_EINVAL, "scene lives on device %d but the current device is %d", sc->device, dev);
+  auto* ws = static_cast<unsigned char*>(workspace);
+  HIP_TRY(hipMemsetAsync(ws + L.counter_off, 0, 512, stream));
+  const size_t lds = lds_bytes(sc, (int)p->precision);
+  if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
+  const int bpc = blocks_per_cu(dev, (int)p->precision, lds);
+  const int cus = device_cus(dev);
+  uint32_t total_units = 0;
+  hipError_t e;
+  if (timer) HIP_TRY(hipEventRecord(timer->start, stream));
+  if (p->precision == RTW_PRECISION_F32) {
+    rtwk::TraceArgs<float> a;
+    fill_args(a, sc->v32, cam, p, ws, L);
+    total_units = a.total_units;
+    const uint32_t want = (total_units + 255) / 256;
+    const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
+    e = rtwk::launch_trace_f32(a, grid, lds, stream, stats);
+  } else {
+    rtwk::TraceArgs<double> a;
+    fill_args(a, sc->v64, cam, p, ws, L);
+    total_units = a.total_units;
+    const uint32_t want = (total_units + 255) / 256;
+    const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
+    e = rtwk::launch_trace_f64(a, grid, lds, stream, stats);
+  }
+  if (e != hipSuccess) return fail(RTW_EHIP, "trace kernel launch: %s", hipGetErrorString(e));
+  if (timer) {
+    HIP_TRY(hipEventRecord(timer->stop, stream));
+    timer->recorded = true;
+  }
+  if (d_rgb) {
+    rtwk::FinalizeArgs f;
+    f.partial = reinterpret_cast<const double*>(ws + L.partial_off);
+    f.rgb = d_rgb;
+    f.mean = d_mean;
+    f.npix = p->row_count * p->width;
+    f.n_chunks = n_chunks(p);
+    f.scale = 1.0 / (double)p->spp;
+    e = rtwk::launch_finalize(f, stream);
+    if (e != hipSuccess) return fail(RTW_EHIP, "finalize kernel launch: %s", hipGetErrorString(e));
+  }
+  return RTW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t rtw_workspace_bytes(const rtw_params* p) {
+  if (validate(p) != RTW_OK) return 0;
+  return ws_layout(p).total;
+}
+
+int rtw_timer_create(rtw_timer* out) {
+  if (!out) return fail(RTW_EINVAL, "timer out is NULL");
+  auto* t = new rtw_timer_s;
+  if (hipEventCreate(&t->start) != hipSuccess || hipEventCreate(&t->stop) != hipSuccess) {
+    delete t;
+    return fail(RTW_EHIP, "hipEventCreate failed");
+  }
+  *out = t;
+  return RTW_OK;
+}
+int rtw_timer_destroy(rtw_timer t) {
+  if (!t) return RTW_OK;
+  (void)hipEventDestroy(t->start);
+  (void)hipEventDestroy(t->stop);
+  delete t;
+  return RTW_OK;
+}
+int rtw_timer_elapsed_ms(rtw_timer t, float* ms) {
+  if (!t || !ms) return fail(RTW_EINVAL, "timer/ms is NULL");
+  if (!t->recorded) return fail(RTW_EINVAL, "timer was never recorded");
+  HIP_TRY(hipEventSynchronize(t->stop));
+  HIP_TRY(hipEventElapsedTime(ms, t->start, t->stop));
+  return RTW_OK;
+}
+
+int rtw_render_device(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
+                      size_t ws_bytes, uint8_t* d_rgb, float* d_mean, void* stream, rtw_timer timer) {
+  if (!sc || !cam) return fail(RTW_EINVAL, "scene/camera is NULL");
+  if (!d_rgb) return fail(RTW_EINVAL, "d_rgb is NULL");
+  const int v = validate(p);
+  if (v != RTW_OK) return v;
+  return launch_all(sc, cam, p, workspace, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, false);
+}
+
+int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
+                      size_t ws_bytes, uint64_t counts_out[4]) {
+  if (!sc || !cam || !counts_out) return fail(RTW_EINVAL, "scene/camera/counts is NULL");
+  const int v = validate(p);
+  if (v != RTW_OK) return v;
+  const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, true);
+  if (r != RTW_OK) return r;
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long st[3] = {0, 0, 0};
+  const WsLayout L = ws_layout(p);
+  HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
+  counts_out[0] = st[0];
+  counts_out[1] = st[1];
+  // every segment tests every sphere; f32 mode skips one small sphere per segment with a skip set
+  counts_out[2] = st[1] * sc->n_static;
+  counts_out[3] = st[1] * sc->n_moving;
+  if (p->precision == RTW_PRECISION_F32) counts_out[2] -= st[2];
+  return RTW_OK;
+}
+
+int rtw_render(const rtw_camera* cam, const rtw_sphere* spheres, uint32_t n, const rtw_material* mats, uint32_t nm,
+               const rtw_params* p, uint8_t* rgb_out, float* mean_out) {
+  if (!cam || !rgb_out) return fail(RTW_EINVAL, "camera/rgb_out is NULL");
+  const int v = validate(p);
+  if (v != RTW_OK) return v;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  const int dev = p->device < 0 ? prev : p->device;
+  if (dev >= ndev) return fail(RTW_EINVAL, "device %d >= device count %d", dev, ndev);
+  HIP_TRY(hipSetDevice(dev));
+  rtw_scene sc = nullptr;
+  int st = rtw_scene_create(spheres, n, mats, nm, &sc);
+  if (st != RTW_OK) {
+    (void)hipSetDevice(prev);
+    return st;
+  }
+  const size_t wsb = ws_layout(p).total;
+  const size_t pix = (size_t)p->row_count * p->width * 3;
+  void *ws = nullptr, *d_rgb = nullptr, *d_mean = nullptr;
+  hipStream_t s = nullptr;
+  st = RTW_OK;
+  if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&d_rgb, pix) != hipSuccess ||
+      (mean_out && hipMalloc(&d_mean, pix * sizeof(float)) != hipSuccess)) {
+    st = fail(RTW_ENOMEM, "rtw_render: device allocation failed");
+  }
+  if (st == RTW_OK && hipStreamCreate(&s) != hipSuccess) st = fail(RTW_EHIP, "hipStreamCreate failed");
+  if (st == RTW_OK)
+    st = launch_all(sc, cam, p, ws, wsb, static_cast<uint8_t*>(d_rgb), static_cast<float*>(d_mean), s, nullptr,
+                    false);
+  if (st == RTW_OK && hipStreamSynchronize(s) != hipSuccess) st = fail(RTW_EHIP, "render failed on the device");
+  if (st == RTW_OK && hipMemcpy(rgb_out, d_rgb, pix, hipMemcpyDeviceToHost) != hipSuccess)
+    st = fail(RTW_EHIP, "copy of rgb_out failed");
+  if (st == RTW_OK && mean_out &&
+      hipMemcpy(mean_out, d_mean, pix * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    st = fail(RTW_EHIP, "copy of mean_out failed");
+  if (s) (void)hipStreamDestroy(s);
+  if (ws) (void)hipFree(ws);
+  if (d_rgb) (void)hipFree(d_rgb);
+  if (d_mean) (void)hipFree(d_mean);
+  rtw_scene_destroy(sc);
+  (void)hipSetDevice(prev);
+  return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// rtw_internal.hpp — device-side scene layout and kernel launch interface,
+// shared by rtw_trace.hip (kernels) and rtw_capi.hip (C ABI).
+//
+// HBM layout of a scene (uploaded once by rtw_scene_create):
+//   sph_R  : n x 8 R    {c0.x, c0.y, c0.z, dc.x, dc.y, dc.z, r*r, r}   (dc = c1 - c0, in f64)
+//   meta   : n x u32    bit0 moving | bit1 wide | bits2-7 time group | bits8-31 material
+//   mat_R  : nm x 8 R   {albedo.xyz, odd.xyz, fuzz, ir}
+//   kind   : nm x u32   rtw_material_kind
+//   tg_R   : ng x 2 R   {t0, t1} per distinct MovingSphere (time0, time1)
+//   wide_d : n x 8 f64  f64 copy of sph (f32 mode solves wide spheres in f64)
+//   tg_d   : ng x 2 f64
+// R = double (precision 0) and float (precision 1) copies are both kept.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtwk {
+
+constexpr uint32_t kMoving = 1u;
+constexpr uint32_t kWide = 2u;
+constexpr uint32_t kMaxTimeGroups = 64;
+constexpr uint32_t kTileW = 8, kTileH = 8;  // 64 pixels = one wave's batch
+constexpr uint32_t kBatch = 64;             // work units fetched per atomic
+constexpr double kWideRadius = 100.0;       // f32 mode: radius >= this -> f64 quadratic
+
+template <typename R>
+struct SceneView {
+  const R* sph;
+  const uint32_t* meta;
+  const R* mat;
+  const uint32_t* kind;
+  const R* tg;
+  const double* wide_d;
+  const double* tg_d;
+  uint32_t n, nm, ng, pad;
+};
+
+template <typename R>
+struct TraceArgs {
+  SceneView<R> sc;
+  R origin[3], horizontal[3], vertical[3], llc[3], cu[3], cv[3];
+  R lens_radius, time0, time1;
+  R bg[3];
+  R tmin;
+  uint32_t W, H, spp, max_depth, chunk, n_chunks;
+  uint32_t row_begin, row_stride, row_count, tiles_x;
+  uint32_t total_units;
+  uint32_t pad;
+  uint64_t seed_base;             // SplitMix64(seed).next()
+  double* partial;                // [n_chunks][row_count*W][3] chunk sums
+  uint32_t* counter;              // work-queue head (zeroed before launch)
+  unsigned long long* stats;      // optional {samples, segments, static, moving} (stats build)
+};
+
+struct FinalizeArgs {
+  const double* partial;
+  uint8_t* rgb;
+  float* mean;
+  uint32_t npix, n_chunks;
+  double scale;  // 1.0 / spp
+};
+
+// Launchers (rtw_trace.hip).  Return hipError_t of the launch.
+hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
+// Resident workgroups per CU for the trace kernel (occupancy query).
+int trace_blocks_per_cu(int precision, size_t lds);
+constexpr int kTraceBlock = 256;
+
+}  // namespace rtwk

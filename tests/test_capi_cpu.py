@@ -1,0 +1,117 @@
+"""The C-ABI library on the CPU: it loads, exports every symbol include/rtw_hip.h
+declares, and its host-side helpers (Camera.init, generateRandomScene, image
+height, argument validation) agree with the oracle.  No compute call here."""
+import ctypes as C
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+from helpers import to_oracle_camera
+
+
+def test_library_exports_every_header_symbol(rtw):
+    syms = rtw.header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(rtw.lib(), s), s
+
+
+def test_abi_version(rtw):
+    assert rtw.abi_version() == 1
+
+
+def test_struct_layouts_match_header(rtw):
+    # sizes of the C structs (x86-64 / gfx950 host ABI)
+    assert C.sizeof(rtw.Material) == 8 + 3 * 8 * 2 + 16
+    assert C.sizeof(rtw.Sphere) == 6 * 8 + 3 * 8 + 8
+    assert C.sizeof(rtw.Camera) == 7 * 24 + 24
+    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12
+
+
+def test_cover_scene_equals_oracle_golden(rtw):
+    with open(os.path.join(GOLDEN, "cover_scene_seed42.json")) as f:
+        g = json.load(f)
+    sph, mats, st = rtw.cover_scene(42)
+    assert st == g["rng_state_after"]
+    assert len(sph) == len(g["spheres"]) and len(mats) == len(g["materials"])
+    for s, gs in zip(sph, g["spheres"]):
+        assert list(s.c0) == gs["c0"] and list(s.c1) == gs["c1"]
+        assert s.radius == gs["radius"] and s.moving == gs["moving"] and s.mat == gs["mat"]
+        if s.moving:
+            assert (s.t0, s.t1) == (gs["t0"], gs["t1"])
+    for m, gm in zip(mats, g["materials"]):
+        assert m.kind == gm["kind"] and list(m.albedo) == gm["albedo"]
+        assert list(m.albedo_odd) == gm["albedo_odd"] and m.fuzz == gm["fuzz"] and m.ir == gm["ir"]
+
+
+@pytest.mark.parametrize("aspect", [16 / 9, 1.5, 1.0])
+def test_camera_init_equals_oracle(rtw, oracle, aspect):
+    a = rtw.cover_camera(aspect)
+    b = oracle.cover_camera(aspect)
+    for n in ("origin", "horizontal", "vertical", "lower_left_corner", "u", "v", "w"):
+        assert list(getattr(a, n)) == list(getattr(b, n)), n
+    assert (a.lens_radius, a.time0, a.time1) == (b.lens_radius, b.time0, b.time1)
+    c = to_oracle_camera(oracle, a)
+    assert list(c.lower_left_corner) == list(b.lower_left_corner)
+
+
+@pytest.mark.parametrize("w,aspect", [(400, 16 / 9), (1200, 16 / 9), (3840, 16 / 9), (600, 1.5), (600, 1.0)])
+def test_image_height(rtw, oracle, w, aspect):
+    assert rtw.image_height(w, aspect) == oracle.image_height(w, aspect)
+
+
+def test_configs_heights(rtw):
+    assert [rtw.image_height(w, 16 / 9) for w in (400, 1200, 3840)] == [225, 675, 2160]
+
+
+@pytest.mark.parametrize("kw,status", [
+    (dict(width=1, height=10, spp=1), -1),
+    (dict(width=10, height=10, spp=0), -1),
+    (dict(width=10, height=10, spp=1, row_stride=0, row_count=1), -1),
+    (dict(width=10, height=10, spp=1, row_begin=9, row_stride=2, row_count=2), -1),
+    (dict(width=5000, height=5000, spp=1), -2),
+    (dict(width=10, height=10, spp=1, precision=7), -1),
+])
+def test_render_rejects_bad_params_before_touching_the_gpu(rtw, kw, status):
+    sph, mats, _ = rtw.cover_scene(42)
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.render(rtw.cover_camera(16 / 9), sph, mats, rtw.make_params(**kw))
+    assert e.value.status == status
+    assert rtw.lib().rtw_last_error()
+
+
+def test_scene_rejects_unsupported_material(rtw):
+    sph, mats, _ = rtw.cover_scene(42)
+    mats[0].kind = rtw.DIFFUSE_LIGHT
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.DeviceScene(sph, mats)
+    assert e.value.status == rtw.RTW_UNSUPPORTED
+
+
+def test_scene_rejects_bad_material_index(rtw):
+    sph, mats, _ = rtw.cover_scene(42)
+    sph[3].mat = 999
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.DeviceScene(sph, mats)
+    assert e.value.status == rtw.RTW_EINVAL
+
+
+def test_workspace_bytes(rtw):
+    p = rtw.make_params(1200, 675, 500)
+    n = rtw.workspace_bytes(p)
+    chunks = (500 + 31) // 32
+    assert n >= chunks * 1200 * 675 * 3 * 8
+    assert n < chunks * 1200 * 675 * 3 * 8 + 4096
+
+
+def test_no_cpu_fallback_without_gpu(rtw):
+    """The product path must fail loudly (RTW_ENODEV) when no GPU is visible."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    sph, mats, _ = rtw.cover_scene(42)
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.render(rtw.cover_camera(16 / 9), sph, mats, rtw.make_params(16, 9, 1))
+    assert e.value.status == rtw.RTW_ENODEV
