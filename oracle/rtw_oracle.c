@@ -538,14 +538,59 @@ void ro_main_cover(uint32_t W, double aspect, uint32_t spp, uint32_t depth, uint
 /* Tier B: the GPU contract (per-sample counter-keyed Xoshiro256++)        */
 /* ===================================================================== */
 
-/* Per-sample RNG key: SplitMix64(seed).next() XOR (pixel << 24 | sample);
- * the sample's generator is Xoshiro256.init(key) (same seeding as
- * DefaultPrng.init).  Keys differ only in their low 48 bits, so the four
- * SplitMix64 states of different samples never coincide. */
-static inline void tierb_seed(uint64_t s[4], uint64_t seed, uint64_t pixel, uint64_t sample) {
+/* Tier-B RNG: Zig std.Random.SplitMix64 used as a COUNTER-BASED generator.
+ * base = SplitMix64.init(seed).next(); sample (pixel p, sample s) owns the
+ * disjoint block of 2^16 consecutive Weyl states starting at
+ *   base + (((p << 24) | s) << 16) * gamma,
+ * i.e. its stream is SplitMix64.init(that state).next(), next(), ...  Every
+ * draw of a frame is a distinct element of ONE SplitMix64 sequence (gamma is
+ * odd, so n -> n*gamma is a bijection), any draw is computable from
+ * (p, s, k) alone, and u64 -> f64/f32 is Zig's Random.float as in Tier A. */
+static inline uint64_t tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample) {
   uint64_t sm = seed;
   const uint64_t base = ro_splitmix64_next(&sm);
-  ro_xoshiro256_seed(s, base ^ ((pixel << 24) | sample));
+  const uint64_t block = ((pixel << 24) | sample) << 16;
+  return base + block * 0x9e3779b97f4a7c15ULL;
+}
+
+/* std/Random.zig float(f64) over a SplitMix64 stream. */
+double ro_sm_f64(uint64_t *st) {
+  const uint64_t rnd = ro_splitmix64_next(st);
+  uint64_t lz = clz64(rnd);
+  if (lz >= 12) {
+    lz = 12;
+    for (;;) {
+      const uint64_t addl = clz64(ro_splitmix64_next(st));
+      lz += addl;
+      if (addl != 64) break;
+      if (lz >= 1022) { lz = 1022; break; }
+    }
+  }
+  const uint64_t bits = ((1022 - lz) << 52) | (rnd & ((1ULL << 52) - 1));
+  double d;
+  memcpy(&d, &bits, 8);
+  return d;
+}
+
+/* std/Random.zig float(f32) over a SplitMix64 stream. */
+float ro_sm_f32(uint64_t *st) {
+  const uint64_t rnd = ro_splitmix64_next(st);
+  uint32_t lz = clz64(rnd);
+  if (lz >= 41) {
+    lz = 41 + clz64(ro_splitmix64_next(st));
+    if (lz == 41 + 64) {
+      const uint32_t r32 = (uint32_t)ro_splitmix64_next(st) | 0x7FFu;
+      lz += (uint32_t)__builtin_clz(r32);
+    }
+  }
+  const uint32_t bits = ((126u - lz) << 23) | ((uint32_t)rnd & ((1u << 23) - 1));
+  float f;
+  memcpy(&f, &bits, 4);
+  return f;
+}
+
+uint64_t ro_tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample) {
+  return tierb_state(seed, pixel, sample);
 }
 
 #define TB_REAL double

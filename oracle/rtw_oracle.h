@@ -14,8 +14,9 @@
  *             rayColor.  (main.zig:295-402, hittable.zig, material.zig,
  *             texture.zig, rand.zig, vec.zig, ray.zig.)
  *   Tier B  — the GPU path's contract: identical per-sample semantics, but the
- *             RNG is the same Xoshiro256++ generator RE-SEEDED per
- *             (seed, pixel, sample) so every sample is independent; the bounce
+ *             RNG is counter-based: Zig's SplitMix64 with its Weyl counter
+ *             split into disjoint 2^16-draw blocks per (seed, pixel, sample),
+ *             so every sample is independent and random-access; the bounce
  *             recursion is evaluated forward (throughput product); samples are
  *             summed per chunk, chunks summed in order.  Precision f64
  *             (reference arithmetic) or f32-hybrid (f32 + f64 for wide spheres).
@@ -89,6 +90,11 @@ void ro_xoshiro256_seed(uint64_t s[4], uint64_t seed);
 uint64_t ro_xoshiro256_next(uint64_t s[4]);
 double ro_random_f64(uint64_t s[4]);
 float ro_random_f32(uint64_t s[4]);
+
+/* Tier-B counter-based stream (see rtw_oracle.c tierb_state). */
+uint64_t ro_tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample);
+double ro_sm_f64(uint64_t *state);
+float ro_sm_f32(uint64_t *state);
 
 /* std/math/pow.zig integer-exponent path (finite x >= 0, integral y > 0). */
 double ro_zig_pow(double x, double y);

@@ -81,6 +81,12 @@ def lib():
         L.ro_random_f64.argtypes = [U64x4]
         L.ro_random_f32.restype = C.c_float
         L.ro_random_f32.argtypes = [U64x4]
+        L.ro_tierb_state.restype = C.c_uint64
+        L.ro_tierb_state.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        L.ro_sm_f64.restype = C.c_double
+        L.ro_sm_f64.argtypes = [C.POINTER(C.c_uint64)]
+        L.ro_sm_f32.restype = C.c_float
+        L.ro_sm_f32.argtypes = [C.POINTER(C.c_uint64)]
         L.ro_zig_pow.restype = C.c_double
         L.ro_zig_pow.argtypes = [C.c_double, C.c_double]
         L.ro_camera_init.argtypes = [C.POINTER(Camera)] + [C.c_double * 3] * 3 + [C.c_double] * 6

@@ -4,8 +4,9 @@
  * TB_REAL = float (precision 1, "f32-hybrid").  TEST INFRASTRUCTURE ONLY.
  *
  * This file IS the written contract the HIP kernel implements:
- *  - per sample: Xoshiro256.init(SplitMix64(seed).next() ^ (pixel<<24 | s)),
- *    pixel = image_row * W + column (image rows top-first);
+ *  - per sample: the counter-based SplitMix64 block of (seed, pixel, s)
+ *    (rtw_oracle.c tierb_state), pixel = image_row * W + column (image rows
+ *    top-first), u64 -> real by Zig's Random.float;
  *  - draw order per sample (main.zig:390-392, main.zig:91-100): u jitter,
  *    v jitter, unit-disk rejection pairs, time; then per bounce the material's
  *    draws (rand.zig:22-40, material.zig:44-85);
@@ -18,7 +19,8 @@
  *  - quantisation exactly main.zig:395-400.
  * f32-hybrid: everything in f32 except spheres with radius >= 100 ("wide"),
  * whose quadratic is solved in f64 from the f64 scene values (the radius-1000
- * ground sphere's c = |oc|^2 - r^2 cancels catastrophically in f32); and a ray
+ * ground sphere's c = |oc|^2 - r^2 cancels catastrophically in f32), its two
+ * roots rounded to f32 before they are compared with anything; and a ray
  * that LEAVES a sphere outward (dot(new_dir, geometric outward normal) > 0)
  * does not test that sphere on its next segment (convex self-skip: exact in
  * real arithmetic, it stops f32 hit points that land a hair inside a sphere
@@ -38,13 +40,13 @@ typedef struct { TBF(R) x, y, z; } TBF(V);
 #define TB_SIN sinf
 #define TB_FABS fabsf
 #define TB_FMIN fminf
-#define TB_RAND01(s) ro_random_f32(s)
+#define TB_RAND01(s) ro_sm_f32(s)
 #else
 #define TB_SQRT sqrt
 #define TB_SIN sin
 #define TB_FABS fabs
 #define TB_FMIN fmin
-#define TB_RAND01(s) ro_random_f64(s)
+#define TB_RAND01(s) ro_sm_f64(s)
 #endif
 
 static inline TBF(V) TBF(mk)(TBF(R) x, TBF(R) y, TBF(R) z) { TBF(V) r = {x, y, z}; return r; }
@@ -60,7 +62,7 @@ static inline TBF(V) TBF(normalized)(TBF(V) v) {
   return (n == (TBF(R))0) ? v : TBF(divs)(v, n);
 }
 static inline TBF(V) TBF(ld)(const double p[3]) { return TBF(mk)((TBF(R))p[0], (TBF(R))p[1], (TBF(R))p[2]); }
-static inline TBF(R) TBF(rrange)(uint64_t s[4], TBF(R) mn, TBF(R) mx) { return mn + TB_RAND01(s) * (mx - mn); }
+static inline TBF(R) TBF(rrange)(uint64_t *s, TBF(R) mn, TBF(R) mx) { return mn + TB_RAND01(s) * (mx - mn); }
 
 typedef struct {
   TBF(V) c0, dc;          /* centre at t0; c1 - c0 (computed in f64, rounded) */
@@ -129,7 +131,7 @@ static inline TBF(V) TBF(center)(const TBF(Sph) *s, TBF(R) time) {
 }
 
 /* rand.zig:22-28 (norm() >= 1 rejection) */
-static inline TBF(V) TBF(in_unit_sphere)(uint64_t s[4], ro_stats *st) {
+static inline TBF(V) TBF(in_unit_sphere)(uint64_t *s, ro_stats *st) {
   for (;;) {
     TBF(V) p;
     p.x = TBF(rrange)(s, -1, 1);
@@ -162,12 +164,13 @@ static inline int TBF(test)(const TBF(Sph) *s, TBF(V) o, TBF(V) d, TBF(R) time, 
     const double disc = hb * hb - ad * c;
     if (disc < 0.0) return 0;
     const double sq = sqrt(disc);
-    double root = (-hb - sq) / ad;
-    if (root < (double)tmin || (double)*tmax < root) {
-      root = (-hb + sq) / ad;
-      if (root < (double)tmin || (double)*tmax < root) return 0;
+    /* roots solved in f64, rounded to f32 before any comparison */
+    float root = (float)((-hb - sq) / ad);
+    if (root < tmin || *tmax < root) {
+      root = (float)((-hb + sq) / ad);
+      if (root < tmin || *tmax < root) return 0;
     }
-    *tmax = (float)root;
+    *tmax = root;
     return 1;
   }
 #endif
@@ -206,8 +209,8 @@ static inline TBF(R) TBF(reflectance)(TBF(R) cosine, TBF(R) ref_idx) {
 /* One sample: returns its colour (the forward restatement of rayColor). */
 static TBF(V) TBF(sample)(const TBF(Scene) *S, const ro_params *p, uint32_t i, uint32_t j,
                           uint64_t pixel, uint32_t s_idx, ro_stats *st) {
-  uint64_t rng[4];
-  tierb_seed(rng, p->seed, pixel, s_idx);
+  uint64_t rng_state = tierb_state(p->seed, pixel, s_idx);
+  uint64_t *rng = &rng_state;
   /* main.zig:390-391 */
   const TBF(R) u = ((TBF(R))i + TB_RAND01(rng)) / ((TBF(R))p->width - 1);
   const TBF(R) v = ((TBF(R))j + TB_RAND01(rng)) / ((TBF(R))p->height - 1);

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -45,8 +46,7 @@ uint64_t splitmix_first(uint64_t seed) {  // SplitMix64.init(seed).next()
 
 struct DevInfo {
   int cus = 0;
-  int bpc[2] = {0, 0};  // blocks per CU per precision (at the LDS size used)
-  size_t bpc_lds[2] = {(size_t)-1, (size_t)-1};
+  std::map<std::pair<int, int>, std::pair<size_t, int>> bpc;  // (precision, var) -> (lds, blocks per CU)
 };
 std::mutex g_dev_mu;
 std::map<int, DevInfo> g_dev;
@@ -61,14 +61,21 @@ int device_cus(int dev) {
   }
   return d.cus;
 }
-int blocks_per_cu(int dev, int prec, size_t lds) {
+int blocks_per_cu(int dev, int prec, size_t lds, int var) {
   std::lock_guard<std::mutex> lk(g_dev_mu);
   auto& d = g_dev[dev];
-  if (d.bpc_lds[prec] != lds) {
-    d.bpc[prec] = rtwk::trace_blocks_per_cu(prec, lds);
-    d.bpc_lds[prec] = lds;
-  }
-  return d.bpc[prec];
+  auto& e = d.bpc[{prec, var}];
+  if (e.second == 0 || e.first != lds) e = {lds, rtwk::trace_blocks_per_cu(prec, lds, var)};
+  return e.second;
+}
+// Kernel tuning variant (rtw_trace.hip VAR bits).  Defaults from the in-process
+// A/B on MI355X (profiles/): f64 = 4 waves/SIMD with scalar sphere
+// records; f32 = 4 waves/SIMD with LDS sphere records.  RTW_VARIANT overrides
+// (development knob).
+int kernel_variant(uint32_t precision) {
+  const char* v = getenv("RTW_VARIANT");
+  if (v && *v) return atoi(v) & 7;
+  return precision == RTW_PRECISION_F32 ? 5 : 4;
 }
 
 }  // namespace
@@ -114,13 +121,13 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   }
   // Distinct (t0, t1) pairs of moving spheres -> time groups.
   std::vector<std::pair<double, double>> groups;
-  std::vector<uint32_t> meta(n);
+  std::vector<uint32_t> meta_orig(n, 0u);
   uint32_t n_moving = 0, n_wide = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const rtw_sphere& s = spheres[i];
     if (s.mat >= nm) return fail(RTW_EINVAL, "sphere %u: material index %u >= %u", i, s.mat, nm);
     if (s.moving > 1) return fail(RTW_EINVAL, "sphere %u: moving flag %u", i, s.moving);
-    uint32_t m = s.mat << 8;
+    uint32_t m = (s.mat << 8) | (i << 20);
     if (s.moving) {
       ++n_moving;
       uint32_t g = 0;
@@ -136,62 +143,97 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
       m |= rtwk::kWide;
       ++n_wide;
     }
-    meta[i] = m;
+    meta_orig[i] = m;
+  }
+  // Table order [static wide | static | moving wide | moving], list order within
+  // each group (rtw_internal.hpp); pos_of[i] = table position of sphere i.
+  std::vector<uint32_t> order;
+  order.reserve(n);
+  for (int grp = 0; grp < 4; ++grp)
+    for (uint32_t i = 0; i < n; ++i) {
+      const bool mv = (meta_orig[i] & rtwk::kMoving) != 0, wd = (meta_orig[i] & rtwk::kWide) != 0;
+      if ((int)mv * 2 + (int)!wd == grp) order.push_back(i);
+    }
+  uint32_t g_end[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    const bool mv = (meta_orig[i] & rtwk::kMoving) != 0, wd = (meta_orig[i] & rtwk::kWide) != 0;
+    for (int grp = (int)mv * 2 + (int)!wd; grp < 4; ++grp) ++g_end[grp];
+  }
+  std::vector<uint32_t> meta(n + 1, 0u), perm(n, 0u);
+  for (uint32_t k = 0; k < n; ++k) {
+    meta[k] = meta_orig[order[k]];
+    perm[order[k]] = k;
   }
   const uint32_t ng = (uint32_t)groups.size();
-  // Host tables.
-  std::vector<double> sph64((size_t)8 * n), mat64((size_t)8 * nm), tg64((size_t)2 * ng);
-  std::vector<float> sph32((size_t)8 * n), mat32((size_t)8 * nm), tg32((size_t)2 * ng);
+  // Host tables (rtw_internal.hpp has the layout).  Reciprocals are correctly
+  // rounded IEEE divisions: the kernel's div_rn needs y = RN(1/b).
+  // sph / meta carry one zero padding record: the sphere loop prefetches k+1.
+  std::vector<double> sph64((size_t)8 * (n + 1), 0.0), rad64(n), mat64((size_t)8 * nm), tg64((size_t)4 * ng);
+  std::vector<float> sph32((size_t)8 * (n + 1), 0.0f), rad32(n), mat32((size_t)8 * nm), tg32((size_t)4 * ng);
   std::vector<uint32_t> kind(nm);
-  for (uint32_t i = 0; i < n; ++i) {
-    const rtw_sphere& s = spheres[i];
+  for (uint32_t i = 0; i < n; ++i) {  // i = table position
+    const rtw_sphere& s = spheres[order[i]];
     const double rec[8] = {s.c0[0], s.c0[1], s.c0[2], s.c1[0] - s.c0[0], s.c1[1] - s.c0[1], s.c1[2] - s.c0[2],
-                           s.radius * s.radius, s.radius};
+                           s.radius * s.radius, 1.0 / s.radius};
     for (int k = 0; k < 8; ++k) sph64[8 * i + k] = rec[k];
     for (int k = 0; k < 6; ++k) sph32[8 * i + k] = (float)rec[k];
     const float rf = (float)s.radius;
     sph32[8 * i + 6] = rf * rf;  // f32 mode: r*r in f32 (tierb_core.h prep)
-    sph32[8 * i + 7] = rf;
+    sph32[8 * i + 7] = 1.0f / rf;
+    rad64[i] = s.radius;
+    rad32[i] = rf;
   }
   for (uint32_t i = 0; i < nm; ++i) {
     const rtw_material& m = mats[i];
+    const bool diel = m.kind == RTW_DIELECTRIC;
     const double rec[8] = {m.albedo[0], m.albedo[1], m.albedo[2], m.albedo_odd[0], m.albedo_odd[1],
-                           m.albedo_odd[2], m.fuzz, m.ir};
+                           m.albedo_odd[2], diel ? 1.0 / m.ir : m.fuzz, m.ir};
     for (int k = 0; k < 8; ++k) {
       mat64[8 * i + k] = rec[k];
       mat32[8 * i + k] = (float)rec[k];
     }
+    if (diel) mat32[8 * i + 6] = 1.0f / (float)m.ir;
     kind[i] = m.kind;
   }
   for (uint32_t g = 0; g < ng; ++g) {
-    tg64[2 * g] = groups[g].first;
-    tg64[2 * g + 1] = groups[g].second;
-    tg32[2 * g] = (float)groups[g].first;
-    tg32[2 * g + 1] = (float)groups[g].second;
+    const double t0 = groups[g].first, t1 = groups[g].second;
+    tg64[4 * g] = t0;
+    tg64[4 * g + 1] = t1;
+    tg64[4 * g + 2] = 1.0 / (t1 - t0);
+    const float f0 = (float)t0, f1 = (float)t1;
+    tg32[4 * g] = f0;
+    tg32[4 * g + 1] = f1;
+    tg32[4 * g + 2] = 1.0f / (f1 - f0);
   }
   // One device allocation, 256-B aligned sub-buffers.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t o_sph64 = 0, s_sph64 = al(sph64.size() * 8 + 8);
-  const size_t o_mat64 = o_sph64 + s_sph64, s_mat64 = al(mat64.size() * 8 + 8);
-  const size_t o_tg64 = o_mat64 + s_mat64, s_tg64 = al(tg64.size() * 8 + 8);
-  const size_t o_sph32 = o_tg64 + s_tg64, s_sph32 = al(sph32.size() * 4 + 4);
-  const size_t o_mat32 = o_sph32 + s_sph32, s_mat32 = al(mat32.size() * 4 + 4);
-  const size_t o_tg32 = o_mat32 + s_mat32, s_tg32 = al(tg32.size() * 4 + 4);
-  const size_t o_meta = o_tg32 + s_tg32, s_meta = al(meta.size() * 4 + 4);
-  const size_t o_kind = o_meta + s_meta, s_kind = al(kind.size() * 4 + 4);
-  const size_t total = o_kind + s_kind;
+  size_t off = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = off;
+    off += al(bytes + 8);
+    return o;
+  };
+  const size_t o_sph64 = place(sph64.size() * 8), o_rad64 = place(rad64.size() * 8);
+  const size_t o_mat64 = place(mat64.size() * 8), o_tg64 = place(tg64.size() * 8);
+  const size_t o_sph32 = place(sph32.size() * 4), o_rad32 = place(rad32.size() * 4);
+  const size_t o_mat32 = place(mat32.size() * 4), o_tg32 = place(tg32.size() * 4);
+  const size_t o_meta = place(meta.size() * 4), o_kind = place(kind.size() * 4), o_perm = place(perm.size() * 4);
+  const size_t total = off;
   std::vector<unsigned char> host(total, 0);
-  auto cp = [&](size_t off, const void* p, size_t bytes) {
-    if (bytes) std::memcpy(host.data() + off, p, bytes);
+  auto cp = [&](size_t o, const void* p, size_t bytes) {
+    if (bytes) std::memcpy(host.data() + o, p, bytes);
   };
   cp(o_sph64, sph64.data(), sph64.size() * 8);
+  cp(o_rad64, rad64.data(), rad64.size() * 8);
   cp(o_mat64, mat64.data(), mat64.size() * 8);
   cp(o_tg64, tg64.data(), tg64.size() * 8);
   cp(o_sph32, sph32.data(), sph32.size() * 4);
+  cp(o_rad32, rad32.data(), rad32.size() * 4);
   cp(o_mat32, mat32.data(), mat32.size() * 4);
   cp(o_tg32, tg32.data(), tg32.size() * 4);
   cp(o_meta, meta.data(), meta.size() * 4);
   cp(o_kind, kind.data(), kind.size() * 4);
+  cp(o_perm, perm.data(), perm.size() * 4);
 
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -211,14 +253,13 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   sc->n_wide = n_wide;
   sc->buf = d;
   auto* b = static_cast<unsigned char*>(d);
-  sc->v64 = {reinterpret_cast<const double*>(b + o_sph64), reinterpret_cast<const uint32_t*>(b + o_meta),
-             reinterpret_cast<const double*>(b + o_mat64), reinterpret_cast<const uint32_t*>(b + o_kind),
-             reinterpret_cast<const double*>(b + o_tg64),  reinterpret_cast<const double*>(b + o_sph64),
-             reinterpret_cast<const double*>(b + o_tg64),  n, nm, ng, 0};
-  sc->v32 = {reinterpret_cast<const float*>(b + o_sph32), reinterpret_cast<const uint32_t*>(b + o_meta),
-             reinterpret_cast<const float*>(b + o_mat32), reinterpret_cast<const uint32_t*>(b + o_kind),
-             reinterpret_cast<const float*>(b + o_tg32),  reinterpret_cast<const double*>(b + o_sph64),
-             reinterpret_cast<const double*>(b + o_tg64), n, nm, ng, 0};
+  auto D = [&](size_t o) { return reinterpret_cast<const double*>(b + o); };
+  auto F = [&](size_t o) { return reinterpret_cast<const float*>(b + o); };
+  auto U = [&](size_t o) { return reinterpret_cast<const uint32_t*>(b + o); };
+  sc->v64 = {D(o_sph64), D(o_rad64), U(o_meta), D(o_mat64), U(o_kind), D(o_tg64), D(o_sph64), D(o_tg64), U(o_perm),
+             n, nm, ng, g_end[0], g_end[1], g_end[2]};
+  sc->v32 = {F(o_sph32), F(o_rad32), U(o_meta), F(o_mat32), U(o_kind), F(o_tg32), D(o_sph64), D(o_tg64), U(o_perm),
+             n, nm, ng, g_end[0], g_end[1], g_end[2]};
   *out = sc;
   return RTW_OK;
 }
@@ -276,7 +317,7 @@ WsLayout ws_layout(const rtw_params* p) {
   w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
   w.counter_off = (w.partial_bytes + 255) & ~(size_t)255;
   w.stats_off = w.counter_off + 256;
-  w.total = w.stats_off + 256;
+  w.total = w.stats_off + 256;  // stats: 32 x u64
   return w;
 }
 
@@ -297,7 +338,13 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
   a.lens_radius = (R)cam->lens_radius;
   a.time0 = (R)cam->time0;
   a.time1 = (R)cam->time1;
-  a.tmin = (R)0.001;
+  a.tmin = (R)0.001;  // rayColor's t_min (main.zig:109)
+  a.inv_w1 = (R)1 / ((R)p->width - (R)1);
+  a.inv_h1 = (R)1 / ((R)p->height - (R)1);
+  // Prefilter bound: root2 <= 2u(1+u)^2 * hb/a < tmin
+  // whenever hb < pre_k * a, u = unit roundoff of R.
+  const double u = sizeof(R) == 8 ? 0x1p-53 : 0x1p-24;
+  a.pre_k = (R)((double)a.tmin / (2.5 * u));
   a.W = p->width;
   a.H = p->height;
   a.spp = p->spp;
@@ -318,11 +365,12 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
 
 size_t lds_bytes(const rtw_scene_s* sc, int prec) {
   const size_t r = prec == 1 ? 4 : 8;
-  return r * (8 * (size_t)sc->n + 8 * (size_t)sc->nm + 2 * (size_t)sc->ng) + 4 * ((size_t)sc->n + sc->nm) + 16;
+  return r * (8 * ((size_t)sc->n + 1) + (size_t)sc->n + 8 * (size_t)sc->nm + 4 * (size_t)sc->ng) +
+         4 * ((size_t)sc->n + 1 + sc->nm + sc->n) + 16;
 }
 
 int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace, size_t ws_bytes,
-               uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, bool stats) {
+               uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode) {
   const WsLayout L = ws_layout(p);
   if (!workspace || ws_bytes < L.total)
     return fail(RTW_EINVAL, "workspace %zu bytes < required %zu", ws_bytes, L.total);
@@ -332,10 +380,11 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   if (dev != sc->device)
     return fail(RTW_EINVAL, "scene lives on device %d but the current device is %d", sc->device, dev);
   auto* ws = static_cast<unsigned char*>(workspace);
-  HIP_TRY(hipMemsetAsync(ws + L.counter_off, 0, 512, stream));
+  HIP_TRY(hipMemsetAsync(ws + L.counter_off, 0, 512, stream));  // queue head + stats
   const size_t lds = lds_bytes(sc, (int)p->precision);
   if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
-  const int bpc = blocks_per_cu(dev, (int)p->precision, lds);
+  const int var = kernel_variant(p->precision);
+  const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);
   const int cus = device_cus(dev);
   uint32_t total_units = 0;
   hipError_t e;
@@ -346,14 +395,14 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
     total_units = a.total_units;
     const uint32_t want = (total_units + 255) / 256;
     const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
-    e = rtwk::launch_trace_f32(a, grid, lds, stream, stats);
+    e = rtwk::launch_trace_f32(a, grid, lds, stream, mode, var);
   } else {
     rtwk::TraceArgs<double> a;
     fill_args(a, sc->v64, cam, p, ws, L);
     total_units = a.total_units;
     const uint32_t want = (total_units + 255) / 256;
     const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
-    e = rtwk::launch_trace_f64(a, grid, lds, stream, stats);
+    e = rtwk::launch_trace_f64(a, grid, lds, stream, mode, var);
   }
   if (e != hipSuccess) return fail(RTW_EHIP, "trace kernel launch: %s", hipGetErrorString(e));
   if (timer) {
@@ -414,7 +463,7 @@ int rtw_render_device(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   if (!d_rgb) return fail(RTW_EINVAL, "d_rgb is NULL");
   const int v = validate(p);
   if (v != RTW_OK) return v;
-  return launch_all(sc, cam, p, workspace, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, false);
+  return launch_all(sc, cam, p, workspace, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, 0);
 }
 
 int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
@@ -422,12 +471,27 @@ int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   if (!sc || !cam || !counts_out) return fail(RTW_EINVAL, "scene/camera/counts is NULL");
   const int v = validate(p);
   if (v != RTW_OK) return v;
-  const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, true);
+  // RTW_PHASE_PROFILE=1: diagnostic build with per-phase s_memtime stamps.
+  const char* prof = getenv("RTW_PHASE_PROFILE");
+  const int mode = (prof && prof[0] == '1') ? 2 : 1;
+  const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, mode);
   if (r != RTW_OK) return r;
   HIP_TRY(hipDeviceSynchronize());
-  unsigned long long st[3] = {0, 0, 0};
+  unsigned long long st[16] = {0};
   const WsLayout L = ws_layout(p);
   HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
+  if (mode == 1 && getenv("RTW_COUNTS_VERBOSE")) {
+    fprintf(stderr, "[rtw counts] samples %llu segments %llu skipped %llu cand_wave_iters %llu cand_lanes %llu "
+            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
+  }
+  if (mode == 2) {
+    const char* names[6] = {"refill", "start_sample", "sphere_loop", "shade", "tail", "loop_top"};
+    unsigned long long tot = 0;
+    for (int i = 0; i < 6; ++i) tot += st[8 + i];
+    for (int i = 0; i < 6; ++i)
+      fprintf(stderr, "[rtw phase] %-13s %6.2f%%  (%llu wave-cycles)\n", names[i], tot ? 100.0 * st[8 + i] / tot : 0.0,
+              st[8 + i]);
+  }
   counts_out[0] = st[0];
   counts_out[1] = st[1];
   // every segment tests every sphere; f32 mode skips one small sphere per segment with a skip set
@@ -467,7 +531,7 @@ int rtw_render(const rtw_camera* cam, const rtw_sphere* spheres, uint32_t n, con
   if (st == RTW_OK && hipStreamCreate(&s) != hipSuccess) st = fail(RTW_EHIP, "hipStreamCreate failed");
   if (st == RTW_OK)
     st = launch_all(sc, cam, p, ws, wsb, static_cast<uint8_t*>(d_rgb), static_cast<float*>(d_mean), s, nullptr,
-                    false);
+                    0);
   if (st == RTW_OK && hipStreamSynchronize(s) != hipSuccess) st = fail(RTW_EHIP, "render failed on the device");
   if (st == RTW_OK && hipMemcpy(rgb_out, d_rgb, pix, hipMemcpyDeviceToHost) != hipSuccess)
     st = fail(RTW_EHIP, "copy of rgb_out failed");

@@ -2,13 +2,18 @@
 // shared by rtw_trace.hip (kernels) and rtw_capi.hip (C ABI).
 //
 // HBM layout of a scene (uploaded once by rtw_scene_create):
-//   sph_R  : n x 8 R    {c0.x, c0.y, c0.z, dc.x, dc.y, dc.z, r*r, r}   (dc = c1 - c0, in f64)
-//   meta   : n x u32    bit0 moving | bit1 wide | bits2-7 time group | bits8-31 material
-//   mat_R  : nm x 8 R   {albedo.xyz, odd.xyz, fuzz, ir}
+//   sph_R  : n x 8 R    {c0.x, c0.y, c0.z, dc.x, dc.y, dc.z, r*r, RN(1/r)}   (dc = c1 - c0, in f64)
+//   rad_R  : n x R      radius
+//   meta   : n x u32    bit0 moving | bit1 wide | bits2-7 time group | bits8-19 material
+//                       | bits20-31 original list index (tie-break)
+//   perm   : n x u32    original list index -> table position
+// Table order: [static wide | static | moving wide | moving] (SceneView g_*
+// offsets), each group in list order; sph / meta carry one padding record.
+//   mat_R  : nm x 8 R   {albedo.xyz, odd.xyz, fuzz (metal) | RN(1/ir) (dielectric), ir}
 //   kind   : nm x u32   rtw_material_kind
-//   tg_R   : ng x 2 R   {t0, t1} per distinct MovingSphere (time0, time1)
+//   tg_R   : ng x 4 R   {t0, t1, RN(1/(t1-t0)), 0} per distinct MovingSphere (time0, time1)
 //   wide_d : n x 8 f64  f64 copy of sph (f32 mode solves wide spheres in f64)
-//   tg_d   : ng x 2 f64
+//   tg_d   : ng x 4 f64
 // R = double (precision 0) and float (precision 1) copies are both kept.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -26,13 +31,16 @@ constexpr double kWideRadius = 100.0;       // f32 mode: radius >= this -> f64 q
 template <typename R>
 struct SceneView {
   const R* sph;
+  const R* rad;
   const uint32_t* meta;
   const R* mat;
   const uint32_t* kind;
   const R* tg;
   const double* wide_d;
   const double* tg_d;
-  uint32_t n, nm, ng, pad;
+  const uint32_t* perm;
+  uint32_t n, nm, ng;
+  uint32_t g_static_wide, g_static, g_moving_wide;  // group ends; the moving group ends at n
 };
 
 template <typename R>
@@ -42,6 +50,8 @@ struct TraceArgs {
   R lens_radius, time0, time1;
   R bg[3];
   R tmin;
+  R inv_w1, inv_h1;               // RN(1/(W-1)), RN(1/(H-1))
+  R pre_k;                        // prefilter bound: tmin / (2.5 * unit roundoff)
   uint32_t W, H, spp, max_depth, chunk, n_chunks;
   uint32_t row_begin, row_stride, row_count, tiles_x;
   uint32_t total_units;
@@ -49,7 +59,7 @@ struct TraceArgs {
   uint64_t seed_base;             // SplitMix64(seed).next()
   double* partial;                // [n_chunks][row_count*W][3] chunk sums
   uint32_t* counter;              // work-queue head (zeroed before launch)
-  unsigned long long* stats;      // optional {samples, segments, static, moving} (stats build)
+  unsigned long long* stats;      // counts {samples, segments, skipped} [0..2]; phase cycles [8..13]
 };
 
 struct FinalizeArgs {
@@ -61,11 +71,13 @@ struct FinalizeArgs {
 };
 
 // Launchers (rtw_trace.hip).  Return hipError_t of the launch.
-hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
-hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+// mode: 0 = product, 1 = counts (segments/samples), 2 = diagnostic phase stamps
+// var: tuning variant (rtw_trace.hip trace_kernel VAR bits)
+hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int var);
+hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int var);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // Resident workgroups per CU for the trace kernel (occupancy query).
-int trace_blocks_per_cu(int precision, size_t lds);
+int trace_blocks_per_cu(int precision, size_t lds, int var);
 constexpr int kTraceBlock = 256;
 
 }  // namespace rtwk

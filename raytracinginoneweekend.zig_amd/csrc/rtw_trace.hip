@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rtw_internal.hpp"
+#include "rtw_math.hpp"
 
 namespace rtwk {
 
@@ -76,86 +77,72 @@ template <typename R>
 __device__ __forceinline__ V3<R> ld3(const R* p) {
   return mk(p[0], p[1], p[2]);
 }
+template <typename R>
+__device__ __forceinline__ V3<R> ld3(const __attribute__((address_space(4))) R* p) {
+  return mk(p[0], p[1], p[2]);
+}
 
 // ------------------------------------------------------------------ RNG --
-// Zig 0.14 std.Random: SplitMix64 seeding of Xoshiro256 (xoshiro256++),
-// Random.float(f64) / float(f32).  Re-seeded per (seed, pixel, sample).
-struct Xo {
-  uint64_t s0, s1, s2, s3;
-};
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+// Counter-based Zig std.Random.SplitMix64: sample (pixel p, sample s) owns the
+// 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its
+// draws are SplitMix64.next() from there, turned into reals by Zig's
+// Random.float (oracle/rtw_oracle.c tierb_state / ro_sm_f64 / ro_sm_f32).
+constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
 __device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
-  st += 0x9e3779b97f4a7c15ULL;
+  st += kGamma;
   uint64_t z = st;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
 }
-__device__ __forceinline__ void xo_seed(Xo& r, uint64_t key) {
-  uint64_t st = key;
-  r.s0 = sm_next(st);
-  r.s1 = sm_next(st);
-  r.s2 = sm_next(st);
-  r.s3 = sm_next(st);
-}
-__device__ __forceinline__ uint64_t xo_next(Xo& r) {
-  const uint64_t res = rotl64(r.s0 + r.s3, 23) + r.s0;
-  const uint64_t t = r.s1 << 17;
-  r.s2 ^= r.s0;
-  r.s3 ^= r.s1;
-  r.s1 ^= r.s2;
-  r.s0 ^= r.s3;
-  r.s2 ^= t;
-  r.s3 = rotl64(r.s3, 45);
-  return res;
-}
 __device__ __forceinline__ uint32_t clz64(uint64_t v) { return v ? (uint32_t)__clzll((long long)v) : 64u; }
 
-__device__ __forceinline__ uint64_t f64_extra_lz(Xo& r) {  // taken with probability 2^-12
-  uint64_t lz = 12;
-  for (;;) {
-    const uint64_t addl = clz64(xo_next(r));
-    lz += addl;
-    if (addl != 64) break;
-    if (lz >= 1022) {
-      lz = 1022;
-      break;
+__device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
+  const uint64_t v = sm_next(st);
+  uint64_t lz = clz64(v);
+  if (__builtin_expect(lz >= 12, 0)) {  // probability 2^-12: extend with more draws
+    lz = 12;
+    for (;;) {
+      const uint64_t addl = clz64(sm_next(st));
+      lz += addl;
+      if (addl != 64) break;
+      if (lz >= 1022) {
+        lz = 1022;
+        break;
+      }
     }
   }
-  return lz;
-}
-__device__ __forceinline__ double rnd_f64(Xo& r) {
-  const uint64_t v = xo_next(r);
-  uint64_t lz = clz64(v);
-  if (__builtin_expect(lz >= 12, 0)) lz = f64_extra_lz(r);
   const uint64_t bits = ((1022 - lz) << 52) | (v & ((1ULL << 52) - 1));
   return __longlong_as_double((long long)bits);
 }
-__device__ __forceinline__ uint32_t f32_extra_lz(Xo& r) {  // probability 2^-41
-  uint32_t lz = 41 + clz64(xo_next(r));
-  if (lz == 41 + 64) lz += (uint32_t)__clz((int)((uint32_t)xo_next(r) | 0x7FFu));
-  return lz;
-}
-__device__ __forceinline__ float rnd_f32(Xo& r) {
-  const uint64_t v = xo_next(r);
+__device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
+  const uint64_t v = sm_next(st);
   uint32_t lz = clz64(v);
-  if (__builtin_expect(lz >= 41, 0)) lz = f32_extra_lz(r);
+  if (__builtin_expect(lz >= 41, 0)) {  // probability 2^-41
+    lz = 41 + clz64(sm_next(st));
+    if (lz == 41 + 64) lz += (uint32_t)__clz((int)((uint32_t)sm_next(st) | 0x7FFu));
+  }
   const uint32_t bits = ((126u - lz) << 23) | ((uint32_t)v & ((1u << 23) - 1));
   return __uint_as_float(bits);
 }
 template <typename R>
-__device__ __forceinline__ R rnd(Xo& r);
+__device__ __forceinline__ R rnd(uint64_t& st);
 template <>
-__device__ __forceinline__ double rnd<double>(Xo& r) {
-  return rnd_f64(r);
+__device__ __forceinline__ double rnd<double>(uint64_t& st) {
+  return rnd_f64(st);
 }
 template <>
-__device__ __forceinline__ float rnd<float>(Xo& r) {
-  return rnd_f32(r);
+__device__ __forceinline__ float rnd<float>(uint64_t& st) {
+  return rnd_f32(st);
 }
 template <typename R>
-__device__ __forceinline__ R rrange(Xo& r, R mn, R mx) {  // rand.zig:18-20
-  return mn + rnd<R>(r) * (mx - mn);
+__device__ __forceinline__ R rrange(uint64_t& st, R mn, R mx) {  // rand.zig:18-20
+  return mn + rnd<R>(st) * (mx - mn);
+}
+// randomReal(-1, 1) = -1 + r*2: r*2 is exact, so one FMA rounds identically.
+template <typename R>
+__device__ __forceinline__ R rrange_m11(uint64_t& st) {
+  return fma(rnd<R>(st), (R)2, (R)-1);
 }
 
 // ------------------------------------------------------------- kernel ----
@@ -167,12 +154,31 @@ template <typename T>
 __device__ __forceinline__ const RTW_CONST T* cptr(const T* p) {
   return (const RTW_CONST T*)(p);
 }
+// A pointer the compiler cannot see through: loads through it are issued
+// where they are written (not hoisted into loop-invariant SGPRs), which keeps
+// the camera block out of the SGPR budget of the sphere loop.
+template <typename T>
+__device__ __forceinline__ const RTW_CONST T* opaque(const RTW_CONST T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// The kernel's only argument (TraceArgs) sits at offset 0 of the kernarg segment.
+template <typename R>
+__device__ __forceinline__ const RTW_CONST TraceArgs<R>* kargs() {
+  return (const RTW_CONST TraceArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
+template <typename R>
+struct Rec {  // one sphere record of the closest-hit loop
+  uint32_t meta;
+  R c[3], dc[3], r2;
+};
 
 template <typename R>
 struct Lane {
   V3<R> o, d, T;
   R time;
-  Xo rng;
+  uint64_t rs;        // SplitMix64 Weyl state of the current sample
   double sx, sy, sz;  // f64 chunk sum (main.zig:388-393 accumulates in f64)
   uint32_t px, ly, c, s, s_end, depth;
   int skip;
@@ -183,19 +189,29 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// v / |v| with the three divisions done against RN(1/|v|) (rtw_math.hpp div_rn).
+template <typename R>
+__device__ __forceinline__ V3<R> normalized_rn(V3<R> v) {  // vec.zig:32-39
+  const R n = sqrt(norm2(v));
+  if (n == (R)0) return v;
+  const R y = (R)1 / n;
+  return mk(rtwm::div_rn(v.x, n, y), rtwm::div_rn(v.y, n, y), rtwm::div_rn(v.z, n, y));
+}
+
 // Camera.getRay (main.zig:91-100) after the u,v jitter (main.zig:390-391).
 template <typename R>
-__device__ __forceinline__ void start_sample(const TraceArgs<R>& A, Lane<R>& L) {
+__device__ __forceinline__ void start_sample(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L) {
+  const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
   const uint32_t y = A.row_begin + L.ly * A.row_stride;  // image row (top-first)
   const uint32_t j = A.H - 1 - y;                        // reference row index
   const uint64_t pixel = (uint64_t)y * A.W + L.px;
-  xo_seed(L.rng, A.seed_base ^ ((pixel << 24) | (uint64_t)L.s));
-  const R u = ((R)L.px + rnd<R>(L.rng)) / ((R)A.W - (R)1);
-  const R v = ((R)j + rnd<R>(L.rng)) / ((R)A.H - (R)1);
+  L.rs = A.seed_base + ((((pixel << 24) | (uint64_t)L.s)) << 16) * kGamma;
+  const R u = rtwm::div_rn((R)L.px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
+  const R v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
   R dx, dy;
   for (;;) {  // rand.zig:30-36; sqrt(x) >= 1 <=> x >= 1 for correctly rounded sqrt
-    dx = rrange<R>(L.rng, (R)-1, (R)1);
-    dy = rrange<R>(L.rng, (R)-1, (R)1);
+    dx = rrange_m11<R>(L.rs);
+    dy = rrange_m11<R>(L.rs);
     if (!(dx * dx + dy * dy + (R)0 * (R)0 >= (R)1)) break;
   }
   const V3<R> rd = mk(dx * A.lens_radius, dy * A.lens_radius, (R)0 * A.lens_radius);
@@ -203,19 +219,23 @@ __device__ __forceinline__ void start_sample(const TraceArgs<R>& A, Lane<R>& L) 
   const V3<R> offset = add(mul(cu, rd.x), mul(cv, rd.y));
   L.d = sub(sub(add(add(ld3(A.llc), mul(ld3(A.horizontal), u)), mul(ld3(A.vertical), v)), org), offset);
   L.o = add(org, offset);
-  L.time = rrange<R>(L.rng, A.time0, A.time1);
+  L.time = rrange<R>(L.rs, A.time0, A.time1);
   L.T = mk((R)1, (R)1, (R)1);
   L.depth = 0;
   L.skip = -1;
 }
 
-// f64 quadratic for a wide sphere in f32 mode (tierb_core.h TBF(test), wide branch).
-__device__ __forceinline__ bool wide_test(const RTW_CONST double* w, uint32_t meta, const RTW_CONST double* tgd, V3<float> o,
-                                          V3<float> d, float time, float tmin, float& tmax) {
+// f64 quadratic for a wide sphere in f32 mode (tierb_core.h TBF(test), wide
+// branch): the roots are solved in f64 and rounded to f32 before any
+// comparison, so a wide sphere competes with the others on f32 roots.
+// Returns false when the line misses (disc < 0); else `root` is the sphere's
+// effective root (root1 if root1 >= tmin, else root2).
+__device__ __forceinline__ bool wide_root(const RTW_CONST double* w, uint32_t meta, const RTW_CONST double* tgd,
+                                          V3<float> o, V3<float> d, float time, float tmin, float& root) {
   double cx = w[0], cy = w[1], cz = w[2];
   if (meta & kMoving) {
     const uint32_t g = (meta >> 2) & 63u;
-    const double fr = ((double)time - tgd[2 * g]) / (tgd[2 * g + 1] - tgd[2 * g]);
+    const double fr = ((double)time - tgd[4 * g]) / (tgd[4 * g + 1] - tgd[4 * g]);
     cx = cx + w[3] * fr;
     cy = cy + w[4] * fr;
     cz = cz + w[5] * fr;
@@ -228,30 +248,95 @@ __device__ __forceinline__ bool wide_test(const RTW_CONST double* w, uint32_t me
   const double disc = hb * hb - ad * c;
   if (disc < 0.0) return false;
   const double sq = sqrt(disc);
-  double root = (-hb - sq) / ad;
-  if (root < (double)tmin || (double)tmax < root) {
-    root = (-hb + sq) / ad;
-    if (root < (double)tmin || (double)tmax < root) return false;
-  }
-  tmax = (float)root;
+  root = (float)((-hb - sq) / ad);
+  if (root < tmin) root = (float)((-hb + sq) / ad);
   return true;
 }
 
-template <typename R, bool F32, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
+// The reference's literal closest-hit loop (hittable.zig:231-244 with
+// Sphere/MovingSphere.hit's root selection), in list order, from LDS tables;
+// used only for lanes that met a NaN in the grouped loops.
+template <typename R, bool F32>
+__device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* l_sph, const R* l_rad,
+                                             const uint32_t* l_meta, const R* l_tg, const uint32_t* l_perm,
+                                             const Lane<R>& L, R a, R tmin, R& tmax, int& hit) {
+  tmax = (R)__builtin_huge_val();
+  hit = -1;
+  for (uint32_t i = 0; i < S.n; ++i) {
+    const uint32_t k = l_perm[i];
+    const uint32_t meta = l_meta[k];
+    if (F32 && (int)k == L.skip) continue;
+    if constexpr (F32) {
+      if (meta & kWide) {
+        float root = 0.0f;
+        if (!wide_root(cptr(S.wide_d) + 8 * k, meta, cptr(S.tg_d), L.o, L.d, L.time, tmin, root)) continue;
+        if (root < tmin || tmax < root) continue;
+        tmax = root;
+        hit = (int)k;
+        continue;
+      }
+    }
+    const R* sp = l_sph + 8 * k;
+    R cx = sp[0], cy = sp[1], cz = sp[2];
+    if (meta & kMoving) {
+      const uint32_t g = (meta >> 2) & 63u;
+      const R fr = (L.time - l_tg[4 * g]) / (l_tg[4 * g + 1] - l_tg[4 * g]);
+      cx = cx + sp[3] * fr;
+      cy = cy + sp[4] * fr;
+      cz = cz + sp[5] * fr;
+    }
+    const R ocx = L.o.x - cx, ocy = L.o.y - cy, ocz = L.o.z - cz;
+    const R hb = ocx * L.d.x + ocy * L.d.y + ocz * L.d.z;
+    const R cc = (ocx * ocx + ocy * ocy + ocz * ocz) - sp[6];
+    const R disc = hb * hb - a * cc;
+    if (disc < (R)0) continue;
+    const R sq = sqrt(disc);
+    R root = (-hb - sq) / a;
+    if (root < tmin || tmax < root) {
+      root = (-hb + sq) / a;
+      if (root < tmin || tmax < root) continue;
+    }
+    tmax = root;
+    hit = (int)k;
+  }
+  (void)l_rad;
+}
+
+// Diagnostic phase stamps (MODE 2 only): s_memtime between phases, summed per
+// wave in SGPRs.  Never part of the product build's timing (rtw_render_counts).
+#define RTW_STAMP(slot)                                                          \
+  if constexpr (MODE == 2) {                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    ph[slot] += t_ - t_last;                                                     \
+    t_last = t_;                                                                 \
+  }
+
+// VAR (tuning variants, selected at launch): bit0 = sphere records from LDS
+// instead of scalar loads; bit1 = unroll the sphere loop by 2; bit2 = ask for
+// 4 waves per SIMD (VGPR budget 128).
+template <typename R, bool F32, int MODE, int VAR>
+__global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(TraceArgs<R> A) {
+  constexpr bool STATS = MODE == 1;
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const SceneView<R> S = A.sc;
   // LDS copies of the per-lane lookup tables (winning sphere, its material).
   R* l_sph = reinterpret_cast<R*>(lds_raw);
-  R* l_mat = l_sph + 8 * S.n;
+  R* l_rad = l_sph + 8 * (S.n + 1);
+  R* l_mat = l_rad + S.n;
   R* l_tg = l_mat + 8 * S.nm;
-  uint32_t* l_meta = reinterpret_cast<uint32_t*>(l_tg + 2 * S.ng);
-  uint32_t* l_kind = l_meta + S.n;
-  for (uint32_t i = threadIdx.x; i < 8 * S.n; i += blockDim.x) l_sph[i] = S.sph[i];
+  uint32_t* l_meta = reinterpret_cast<uint32_t*>(l_tg + 4 * S.ng);
+  uint32_t* l_kind = l_meta + S.n + 1;
+  uint32_t* l_perm = l_kind + S.nm;  // original list index -> table position
+  for (uint32_t i = threadIdx.x; i < 8 * (S.n + 1); i += blockDim.x) l_sph[i] = S.sph[i];
+  for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) l_rad[i] = S.rad[i];
   for (uint32_t i = threadIdx.x; i < 8 * S.nm; i += blockDim.x) l_mat[i] = S.mat[i];
-  for (uint32_t i = threadIdx.x; i < 2 * S.ng; i += blockDim.x) l_tg[i] = S.tg[i];
-  for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) l_meta[i] = S.meta[i];
+  for (uint32_t i = threadIdx.x; i < 4 * S.ng; i += blockDim.x) l_tg[i] = S.tg[i];
+  for (uint32_t i = threadIdx.x; i < S.n + 1; i += blockDim.x) l_meta[i] = S.meta[i];
   for (uint32_t i = threadIdx.x; i < S.nm; i += blockDim.x) l_kind[i] = S.kind[i];
+  for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) l_perm[i] = S.perm[i];
   __syncthreads();
 
   const uint32_t lid = lane_id();
@@ -263,14 +348,20 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
   Lane<R> L;
   L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
   L.sx = L.sy = L.sz = 0.0;
+  L.rs = 0;
   L.skip = -1;
   bool have_unit = false;  // lane owns a (pixel, chunk) unit
   bool have_ray = false;   // lane has a live path
   bool done = false;       // queue exhausted for this lane
   uint32_t qnext = 0, qend = 0;  // wave-uniform batch [qnext, qend)
   unsigned long long st_samples = 0, st_segments = 0, st_skipped = 0;
+  unsigned long long st_candwave = 0, st_candlane = 0, st_disc = 0, st_iters = 0, st_wave_iters = 0;
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t t_last = 0;
+  if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last)::"memory");
 
   for (;;) {
+    RTW_STAMP(5)
     // ---- 1. take units for lanes that need one (wave-uniform control) ----
     const bool need = !have_unit && !done;
     const uint64_t needmask = __ballot(need);
@@ -319,12 +410,14 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
       if (__all(done)) break;
       continue;
     }
+    RTW_STAMP(0)
 
-    // ---- 2. new samples: per-sample RNG + camera ray ----
+    // ---- 2. new samples: per-sample RNG block + camera ray ----
     if (have_unit && !have_ray) {
-      start_sample<R>(A, L);
+      start_sample<R>(kargs<R>(), L);
       have_ray = true;
     }
+    RTW_STAMP(1)
 
     // ---- 3. one bounce segment ----
     if (have_ray) {
@@ -334,65 +427,133 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
         ended = true;
       } else {
         if (STATS) st_segments++;
+        if constexpr (STATS) {
+          if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_wave_iters++;
+        }
         const R a = norm2(L.d);
+        const R inv_a = (R)1 / a;          // RN(1/a): roots via div_rn
+        const R pre_lim = A.pre_k * a;     // "both roots behind" prefilter bound
         R tmax = kInf;
         int hit = -1;
         int tg_cur = -1;
         R frac = (R)0;
-        // HittableList.hit (hittable.zig:231-244): every lane tests sphere k
-        // together; the record comes through scalar loads.
         const RTW_CONST uint32_t* c_meta = cptr(S.meta);
         const RTW_CONST R* c_sph = cptr(S.sph);
         const RTW_CONST R* c_tg = cptr(S.tg);
-        for (uint32_t k = 0; k < S.n; ++k) {
-          const uint32_t meta = c_meta[k];
-          if constexpr (F32) {
-            if (meta & kWide) {
-              float tm = tmax;
-              if ((int)k != L.skip && wide_test(cptr(S.wide_d) + 8 * k, meta, cptr(S.tg_d), L.o, L.d, L.time, tmin, tm)) {
-                tmax = tm;
-                hit = (int)k;
-              }
-              continue;
-            }
+        // HittableList.hit (hittable.zig:231-244): every lane tests sphere k
+        // together; the record comes through scalar loads.
+        // Closest hit.  The reference's sequential HittableList.hit returns the
+        // sphere of minimal effective root (root1 if root1 >= tmin, else root2;
+        // root2 >= root1 always), ties to the LAST in list order — an
+        // order-independent rule.  So the table is
+        // grouped [static-wide | static | moving-wide | moving] and each group
+        // runs as its own branch-free loop; ties compare original indices.
+        int hit_orig = -1;
+        bool nan_seen = false;
+        auto accept = [&](R root, int pos, int orig) {
+          if (root != root) nan_seen = true;  // NaN: sequential fallback below
+          if (!(root < tmin) & ((root < tmax) | ((root == tmax) & (orig > hit_orig)))) {
+            tmax = root;
+            hit = pos;
+            hit_orig = orig;
           }
-          const RTW_CONST R* sp = c_sph + 8 * k;
-          R cx = sp[0], cy = sp[1], cz = sp[2];
-          if (meta & kMoving) {  // MovingSphere.center (hittable.zig:219-221)
-            const int g = (int)((meta >> 2) & 63u);
-            if (g != tg_cur) {
-              tg_cur = g;
-              frac = (L.time - c_tg[2 * g]) / (c_tg[2 * g + 1] - c_tg[2 * g]);
-            }
-            cx = cx + sp[3] * frac;
-            cy = cy + sp[4] * frac;
-            cz = cz + sp[5] * frac;
-          }
+        };
+        auto test = [&](uint32_t k, uint32_t meta, R cx, R cy, R cz, R r2) {
           const R ocx = L.o.x - cx, ocy = L.o.y - cy, ocz = L.o.z - cz;
           const R hb = ocx * L.d.x + ocy * L.d.y + ocz * L.d.z;
-          const R cc = (ocx * ocx + ocy * ocy + ocz * ocz) - sp[6];
+          const R cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
           const R disc = hb * hb - a * cc;
-          bool cand = !(disc < (R)0);
-          if (F32) cand = cand && ((int)k != L.skip);
+          // Candidate unless disc < 0, or provably both roots < tmin: origin
+          // outside (cc > 0) and sphere behind (hb > 0) give root1 <= 0 and
+          // root2 <= ~2u*hb/a < tmin while hb < pre_k*a.
+          // (bitwise &, | : no short-circuit branches in the hot loop)
+          const bool pre = (hb > (R)0) & (cc > (R)0) & (hb < pre_lim);
+          bool cand = ((disc >= (R)0) & !pre) | (disc != disc);
+          if (F32) cand = cand & ((int)k != L.skip);
+          if constexpr (STATS) {
+            const uint64_t cm = __ballot(cand);
+            if (cm && lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_candwave++;
+            st_candlane += cand ? 1 : 0;
+            st_disc += !(disc < (R)0) ? 1 : 0;
+          }
           if (cand) {
             const R sq = sqrt(disc);
-            R root = (-hb - sq) / a;
-            bool ok = !(root < tmin || tmax < root);
-            if (!ok) {
-              root = (-hb + sq) / a;
-              ok = !(root < tmin || tmax < root);
+            R root = rtwm::div_rn(-hb - sq, a, inv_a);
+            if (root < tmin) root = rtwm::div_rn(-hb + sq, a, inv_a);
+            accept(root, (int)k, (int)(meta >> 20));
+          }
+        };
+        auto rec_at = [&](uint32_t k) {
+          Rec<R> r;
+          if constexpr (VAR & 1) {
+            const R* sp = l_sph + 8 * k;
+            r.meta = l_meta[k];
+            r.c[0] = sp[0], r.c[1] = sp[1], r.c[2] = sp[2], r.dc[0] = sp[3], r.dc[1] = sp[4], r.dc[2] = sp[5];
+            r.r2 = sp[6];
+          } else {
+            const RTW_CONST R* sp = c_sph + 8 * k;
+            r.meta = c_meta[k];
+            r.c[0] = sp[0], r.c[1] = sp[1], r.c[2] = sp[2], r.dc[0] = sp[3], r.dc[1] = sp[4], r.dc[2] = sp[5];
+            r.r2 = sp[6];
+          }
+          return r;
+        };
+        // f32 mode: wide spheres (radius >= 100), solved in f64.
+        if constexpr (F32) {
+          auto wide_range = [&](uint32_t b, uint32_t e) {
+            for (uint32_t k = b; k < e; ++k) {
+              const uint32_t meta = c_meta[k];
+              float root = 0.0f;
+              if ((int)k != L.skip && wide_root(cptr(S.wide_d) + 8 * k, meta, cptr(S.tg_d), L.o, L.d, L.time, tmin, root))
+                accept(root, (int)k, (int)(meta >> 20));
             }
-            if (ok) {
-              tmax = root;
-              hit = (int)k;
+          };
+          wide_range(0, S.g_static_wide);
+          wide_range(S.g_static, S.g_moving_wide);
+        }
+        // static spheres: records stream one step ahead (padding record at the end)
+        {
+          const uint32_t b = F32 ? S.g_static_wide : 0u, e = S.g_static;
+          if (b < e) {
+            Rec<R> cur = rec_at(b);
+#pragma unroll(((VAR & 2) ? 2 : 1))
+            for (uint32_t k = b; k < e; ++k) {
+              const Rec<R> nxt = rec_at(k + 1);
+              test(k, cur.meta, cur.c[0], cur.c[1], cur.c[2], cur.r2);
+              cur = nxt;
             }
           }
         }
+        // moving spheres: centre(t) = c0 + (c1 - c0) * frac (hittable.zig:219-221)
+        {
+          const uint32_t b = F32 ? S.g_moving_wide : S.g_static, e = S.n;
+          if (b < e) {
+            Rec<R> cur = rec_at(b);
+#pragma unroll(((VAR & 2) ? 2 : 1))
+            for (uint32_t k = b; k < e; ++k) {
+              const Rec<R> nxt = rec_at(k + 1);
+              const int g = (int)((cur.meta >> 2) & 63u);
+              if (g != tg_cur) {  // wave-uniform: recomputed only when the time group changes
+                tg_cur = g;
+                frac = rtwm::div_rn(L.time - c_tg[4 * g], c_tg[4 * g + 1] - c_tg[4 * g], c_tg[4 * g + 2]);
+              }
+              test(k, cur.meta, cur.c[0] + cur.dc[0] * frac, cur.c[1] + cur.dc[1] * frac, cur.c[2] + cur.dc[2] * frac,
+                   cur.r2);
+              cur = nxt;
+            }
+          }
+        }
+        // A NaN anywhere makes the reference's acceptance order-dependent:
+        // redo such lanes with its literal sequential loop.
+        if (__builtin_expect(__any(nan_seen), 0)) {
+          if (nan_seen) seq_closest_hit<R, F32>(S, l_sph, l_rad, l_meta, l_tg, l_perm, L, a, tmin, tmax, hit);
+        }
         if (STATS && L.skip >= 0) st_skipped++;
+        RTW_STAMP(2)
 
         if (hit < 0) {  // miss: background (main.zig:109-112)
           ended = true;
-          col = mulv(L.T, ld3(A.bg));
+          col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
         } else {
           // Hit record of the winner (hittable.zig:118-128, :189-198).
           const R* sp = l_sph + 8 * hit;
@@ -401,45 +562,47 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
           V3<R> center = ld3(sp);
           if (meta & kMoving) {
             const uint32_t g = (meta >> 2) & 63u;
-            const R fr = (L.time - l_tg[2 * g]) / (l_tg[2 * g + 1] - l_tg[2 * g]);
+            const R fr = rtwm::div_rn(L.time - l_tg[4 * g], l_tg[4 * g + 1] - l_tg[4 * g], l_tg[4 * g + 2]);
             center = add(center, mul(ld3(sp + 3), fr));
           }
-          const V3<R> outward = divs(sub(p, center), sp[7]);
+          const R rad = l_rad[hit], inv_r = sp[7];
+          const V3<R> q = sub(p, center);
+          const V3<R> outward = mk(rtwm::div_rn(q.x, rad, inv_r), rtwm::div_rn(q.y, rad, inv_r),
+                                   rtwm::div_rn(q.z, rad, inv_r));
           const bool front = dot(outward, L.d) < (R)0;
           const V3<R> normal = front ? outward : mul(outward, (R)-1);
-          const uint32_t mi = meta >> 8;
+          const uint32_t mi = (meta >> 8) & 0xFFFu;
           const uint32_t kind = l_kind[mi];
           const R* mp = l_mat + 8 * mi;
           // Material.scatter (material.zig:22-29), lanes of one kind together.
           V3<R> ud = L.d;
-          if (kind >= 2u) ud = normalized(L.d);  // metal / dielectric
+          if (kind >= 2u) ud = normalized_rn(L.d);  // metal / dielectric
           V3<R> rs = mk((R)0, (R)0, (R)0);
           if (kind <= 2u) {  // randomPointInUnitSphere (rand.zig:22-28)
             for (;;) {
-              rs.x = rrange<R>(L.rng, (R)-1, (R)1);
-              rs.y = rrange<R>(L.rng, (R)-1, (R)1);
-              rs.z = rrange<R>(L.rng, (R)-1, (R)1);
+              rs.x = rrange_m11<R>(L.rs);
+              rs.y = rrange_m11<R>(L.rs);
+              rs.z = rrange_m11<R>(L.rs);
               if (!(norm2(rs) >= (R)1)) break;
             }
           }
           V3<R> ndir, att;
           bool absorbed = false;
           if (kind <= 1u) {  // Lambertian (material.zig:44-52)
-            ndir = add(normal, normalized(rs));
+            ndir = add(normal, normalized_rn(rs));
             if (fabs(ndir.x) < (R)1e-8 && fabs(ndir.y) < (R)1e-8 && fabs(ndir.z) < (R)1e-8) ndir = normal;
             att = ld3(mp);
-            if (kind == 1u) {  // CheckerTexture.value (texture.zig:79-82)
-              const R sines = sin((R)10 * p.x) * sin((R)10 * p.y) * sin((R)10 * p.z);
-              if (sines < (R)0) att = ld3(mp + 3);
-            }
+            // CheckerTexture.value (texture.zig:79-82): only the sign matters.
+            if (kind == 1u && rtwm::checker_odd((double)((R)10 * p.x), (double)((R)10 * p.y), (double)((R)10 * p.z)))
+              att = ld3(mp + 3);
           } else if (kind == 2u) {  // Metal (material.zig:59-65)
             const V3<R> refl = sub(ud, mul(normal, (R)2 * dot(ud, normal)));
             ndir = add(refl, mul(rs, mp[6]));
             att = ld3(mp);
             absorbed = !(dot(refl, normal) > (R)0);
-          } else {  // Dielectric (material.zig:72-91)
+          } else {  // Dielectric (material.zig:72-91); mp[6] = RN(1/ir)
             const R ir = mp[7];
-            const R ratio = front ? (R)1 / ir : ir;
+            const R ratio = front ? mp[6] : ir;
             const R cos_t = fmin(dot(mul(ud, (R)-1), normal), (R)1);
             const R sin_t = sqrt((R)1 - cos_t * cos_t);
             bool refr = false;
@@ -449,7 +612,7 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
               const R x = (R)1 - cos_t;
               const R x2 = x * x;
               const R refl_p = r1 + ((R)1 - r1) * (x * (x2 * x2));  // Zig pow(x, 5.0)
-              refr = refl_p < rnd<R>(L.rng);
+              refr = refl_p < rnd<R>(L.rs);
             }
             if (refr) {  // refract (material.zig:116-121)
               const R ct = fmin(dot(mul(ud, (R)-1), normal), (R)1);
@@ -472,6 +635,7 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
           }
         }
       }
+      RTW_STAMP(3)
       if (ended) {
         L.sx += (double)col.x;
         L.sy += (double)col.y;
@@ -493,6 +657,15 @@ __global__ void __launch_bounds__(kTraceBlock) trace_kernel(TraceArgs<R> A) {
     atomicAdd(A.stats + 0, st_samples);
     atomicAdd(A.stats + 1, st_segments);
     atomicAdd(A.stats + 2, st_skipped);
+    atomicAdd(A.stats + 3, st_candwave);
+    atomicAdd(A.stats + 4, st_candlane);
+    atomicAdd(A.stats + 5, st_disc);
+    atomicAdd(A.stats + 6, st_wave_iters);
+  }
+  if constexpr (MODE == 2) {
+    RTW_STAMP(4)
+    if (lid == 0)
+      for (int i = 0; i < 6; ++i) atomicAdd(A.stats + 8 + i, (unsigned long long)ph[i]);
   }
 }
 
@@ -516,20 +689,38 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinalizeArgs F) {
   }
 }
 
-template <typename R, bool F32>
-static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats) {
-  if (stats)
-    hipLaunchKernelGGL((trace_kernel<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+template <typename R, bool F32, int VAR>
+static void launch_var(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
+  if (mode == 1)
+    hipLaunchKernelGGL((trace_kernel<R, F32, 1, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (mode == 2)
+    hipLaunchKernelGGL((trace_kernel<R, F32, 2, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else
-    hipLaunchKernelGGL((trace_kernel<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+    hipLaunchKernelGGL((trace_kernel<R, F32, 0, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+}
+template <typename R, bool F32>
+static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
+                               int var) {
+  switch (var & 7) {
+    case 1: launch_var<R, F32, 1>(a, grid, lds, s, mode); break;
+    case 2: launch_var<R, F32, 2>(a, grid, lds, s, mode); break;
+    case 3: launch_var<R, F32, 3>(a, grid, lds, s, mode); break;
+    case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
+    case 5: launch_var<R, F32, 5>(a, grid, lds, s, mode); break;
+    case 6: launch_var<R, F32, 6>(a, grid, lds, s, mode); break;
+    case 7: launch_var<R, F32, 7>(a, grid, lds, s, mode); break;
+    default: launch_var<R, F32, 0>(a, grid, lds, s, mode); break;
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats) {
-  return launch_trace<double, false>(a, grid, lds, s, stats);
+hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
+                            int var) {
+  return launch_trace<double, false>(a, grid, lds, s, mode, var);
 }
-hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats) {
-  return launch_trace<float, true>(a, grid, lds, s, stats);
+hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
+                            int var) {
+  return launch_trace<float, true>(a, grid, lds, s, mode, var);
 }
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   const uint32_t grid = min((a.npix + 255u) / 256u, 4096u);
@@ -537,15 +728,23 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-int trace_blocks_per_cu(int precision, size_t lds) {
+template <typename R, bool F32, int VAR>
+static int occ(size_t lds) {
   int nb = 0;
-  hipError_t e;
-  if (precision == 1)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trace_kernel<float, true, false>, kTraceBlock, lds);
-  else
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trace_kernel<double, false, false>, kTraceBlock, lds);
-  if (e != hipSuccess || nb <= 0) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trace_kernel<R, F32, 0, VAR>, kTraceBlock, lds) != hipSuccess)
+    nb = 0;
   return nb;
+}
+int trace_blocks_per_cu(int precision, size_t lds, int var) {
+  int nb = 0;
+  switch (var & 7) {
+#define RTW_OCC_CASE(v) \
+  case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
+    RTW_OCC_CASE(0) RTW_OCC_CASE(1) RTW_OCC_CASE(2) RTW_OCC_CASE(3)
+    RTW_OCC_CASE(4) RTW_OCC_CASE(5) RTW_OCC_CASE(6) RTW_OCC_CASE(7)
+#undef RTW_OCC_CASE
+  }
+  return nb > 0 ? nb : 1;
 }
 
 }  // namespace rtwk

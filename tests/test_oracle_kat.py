@@ -103,3 +103,23 @@ def test_sqrt_threshold_equivalence():
     assert math.sqrt(below) < 1.0
     fb = np.nextafter(np.float32(1.0), np.float32(0.0))
     assert np.sqrt(fb) < np.float32(1.0)
+
+
+def test_tierb_counter_stream(oracle, kat):
+    """Tier-B RNG: SplitMix64 state base + (((p << 24) | s) << 16) * gamma."""
+    import ctypes as C
+    L = oracle.lib()
+    gamma = 0x9E3779B97F4A7C15
+    base = oracle.splitmix64_seq(42, 1)[0]
+    for p, s in [(0, 0), (1234, 77), (8294399, 1999)]:
+        want = (base + ((((p << 24) | s) << 16) * gamma)) % (1 << 64)
+        assert L.ro_tierb_state(42, p, s) == want
+    assert L.ro_tierb_state(42, 1234, 77) == kat["tierb_state_42_p1234_s77"]
+    st = C.c_uint64(L.ro_tierb_state(42, 1234, 77))
+    assert [float.hex(L.ro_sm_f64(C.byref(st))) for _ in range(6)] == kat["tierb_42_p1234_s77_f64_hex"]
+    # the stream IS SplitMix64.init(state).next(): check against the Python restatement
+    import rtw_oracle_py as P
+    g = P.SplitMix64(L.ro_tierb_state(42, 1234, 77))
+    st = C.c_uint64(L.ro_tierb_state(42, 1234, 77))
+    for _ in range(100):
+        assert L.ro_splitmix64_next(C.byref(st)) == g.next()
