@@ -97,23 +97,28 @@ __device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
 }
 __device__ __forceinline__ uint32_t clz64(uint64_t v) { return v ? (uint32_t)__clzll((long long)v) : 64u; }
 
-__device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
-  const uint64_t v = sm_next(st);
-  uint64_t lz = clz64(v);
-  if (__builtin_expect(lz >= 12, 0)) {  // probability 2^-12: extend with more draws
-    lz = 12;
-    for (;;) {
-      const uint64_t addl = clz64(sm_next(st));
-      lz += addl;
-      if (addl != 64) break;
-      if (lz >= 1022) {
-        lz = 1022;
-        break;
-      }
+__device__ __forceinline__ uint32_t f64_long_lz(uint64_t& st) {  // probability 2^-12 per draw
+  uint32_t lz = 12;
+  for (;;) {
+    const uint32_t addl = clz64(sm_next(st));
+    lz += addl;
+    if (addl != 64) break;
+    if (lz >= 1022) {
+      lz = 1022;
+      break;
     }
   }
-  const uint64_t bits = ((1022 - lz) << 52) | (v & ((1ULL << 52) - 1));
-  return __longlong_as_double((long long)bits);
+  return lz;
+}
+__device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
+  const uint64_t v = sm_next(st);
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  // exponent = 1022 - clz(v); mantissa = low 52 bits.  Common case: the
+  // leading one is in the top 12 bits, i.e. in `hi`.
+  uint32_t lz = (uint32_t)__clz((int)hi);
+  if (__builtin_expect(hi < 0x00100000u, 0)) lz = f64_long_lz(st);
+  const uint32_t bhi = ((1022u - lz) << 20) | (hi & 0x000FFFFFu);
+  return __hiloint2double((int)bhi, (int)lo);
 }
 __device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
   const uint64_t v = sm_next(st);
@@ -466,21 +471,25 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
           // Candidate unless disc < 0, or provably both roots < tmin: origin
           // outside (cc > 0) and sphere behind (hb > 0) give root1 <= 0 and
           // root2 <= ~2u*hb/a < tmin while hb < pre_k*a.
-          // (bitwise &, | : no short-circuit branches in the hot loop)
-          const bool pre = (hb > (R)0) & (cc > (R)0) & (hb < pre_lim);
-          bool cand = ((disc >= (R)0) & !pre) | (disc != disc);
-          if (F32) cand = cand & ((int)k != L.skip);
-          if constexpr (STATS) {
-            const uint64_t cm = __ballot(cand);
-            if (cm && lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_candwave++;
-            st_candlane += cand ? 1 : 0;
-            st_disc += !(disc < (R)0) ? 1 : 0;
-          }
-          if (cand) {
-            const R sq = sqrt(disc);
-            R root = rtwm::div_rn(-hb - sq, a, inv_a);
-            if (root < tmin) root = rtwm::div_rn(-hb + sq, a, inv_a);
-            accept(root, (int)k, (int)(meta >> 20));
+          // One compare on the hot path; ~97 % of tests end here.  A NaN disc
+          // also enters (reference: `disc < 0` is false for NaN).
+          if (!(disc < (R)0)) {
+            // (bitwise &: no short-circuit branches)
+            const bool pre = (hb > (R)0) & (cc > (R)0) & (hb < pre_lim);
+            bool cand = !pre;
+            if (F32) cand = cand & ((int)k != L.skip);
+            if constexpr (STATS) {
+              const uint64_t cm = __ballot(cand);
+              if (cm && lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_candwave++;
+              st_candlane += cand ? 1 : 0;
+              st_disc += 1;
+            }
+            if (cand) {
+              const R sq = sqrt(disc);
+              R root = rtwm::div_rn(-hb - sq, a, inv_a);
+              if (root < tmin) root = rtwm::div_rn(-hb + sq, a, inv_a);
+              accept(root, (int)k, (int)(meta >> 20));
+            }
           }
         };
         auto rec_at = [&](uint32_t k) {
