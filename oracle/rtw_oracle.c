@@ -553,14 +553,22 @@ static inline uint64_t tierb_state(uint64_t seed, uint64_t pixel, uint64_t sampl
   return base + block * 0x9e3779b97f4a7c15ULL;
 }
 
-/* std/Random.zig float(f64) over a SplitMix64 stream. */
+/* Tier-B reals: Zig's Random.float over the counter stream, with ONE rule
+ * change that makes every draw exactly one Weyl step (so draw k of a sample is
+ * random-access): when the draw's u64 has >= 12 (f64) / >= 41 (f32) leading
+ * zeros, Zig takes further u64s from the same generator; here they come from
+ * the draw's own extension stream SplitMix64.init(state_of_draw ^ kTierBExt).
+ * Probability 2^-12 / 2^-41 per draw; the value distribution is unchanged. */
+#define kTierBExt 0x5851F42D4C957F2DULL
+
 double ro_sm_f64(uint64_t *st) {
   const uint64_t rnd = ro_splitmix64_next(st);
   uint64_t lz = clz64(rnd);
   if (lz >= 12) {
+    uint64_t ext = *st ^ kTierBExt;
     lz = 12;
     for (;;) {
-      const uint64_t addl = clz64(ro_splitmix64_next(st));
+      const uint64_t addl = clz64(ro_splitmix64_next(&ext));
       lz += addl;
       if (addl != 64) break;
       if (lz >= 1022) { lz = 1022; break; }
@@ -572,14 +580,14 @@ double ro_sm_f64(uint64_t *st) {
   return d;
 }
 
-/* std/Random.zig float(f32) over a SplitMix64 stream. */
 float ro_sm_f32(uint64_t *st) {
   const uint64_t rnd = ro_splitmix64_next(st);
   uint32_t lz = clz64(rnd);
   if (lz >= 41) {
-    lz = 41 + clz64(ro_splitmix64_next(st));
+    uint64_t ext = *st ^ kTierBExt;
+    lz = 41 + clz64(ro_splitmix64_next(&ext));
     if (lz == 41 + 64) {
-      const uint32_t r32 = (uint32_t)ro_splitmix64_next(st) | 0x7FFu;
+      const uint32_t r32 = (uint32_t)ro_splitmix64_next(&ext) | 0x7FFu;
       lz += (uint32_t)__builtin_clz(r32);
     }
   }

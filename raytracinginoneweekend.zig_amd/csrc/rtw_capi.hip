@@ -69,13 +69,13 @@ int blocks_per_cu(int dev, int prec, size_t lds, int var) {
   return e.second;
 }
 // Kernel tuning variant (rtw_trace.hip VAR bits).  Defaults from the in-process
-// A/B on MI355X (profiles/): f64 = 4 waves/SIMD with scalar sphere
-// records; f32 = 4 waves/SIMD with LDS sphere records.  RTW_VARIANT overrides
-// (development knob).
+// A/B on MI355X (profiles/): both use scalar sphere records and
+// coop_reject for the unit-ball point; f64 at 4 waves/SIMD (128 VGPRs), f32 at
+// 5 waves/SIMD (96 VGPRs).  RTW_VARIANT overrides (development knob).
 int kernel_variant(uint32_t precision) {
   const char* v = getenv("RTW_VARIANT");
-  if (v && *v) return atoi(v) & 7;
-  return precision == RTW_PRECISION_F32 ? 5 : 4;
+  if (v && *v) return atoi(v);
+  return precision == RTW_PRECISION_F32 ? 8 : 4;
 }
 
 }  // namespace
@@ -365,7 +365,7 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
 
 size_t lds_bytes(const rtw_scene_s* sc, int prec) {
   const size_t r = prec == 1 ? 4 : 8;
-  return r * (8 * ((size_t)sc->n + 1) + (size_t)sc->n + 8 * (size_t)sc->nm + 4 * (size_t)sc->ng) +
+  return rtwk::kCoopLdsBytes + r * (8 * ((size_t)sc->n + 1) + (size_t)sc->n + 8 * (size_t)sc->nm + 4 * (size_t)sc->ng) +
          4 * ((size_t)sc->n + 1 + sc->nm + sc->n) + 16;
 }
 

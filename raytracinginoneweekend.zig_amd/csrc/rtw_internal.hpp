@@ -79,5 +79,7 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // Resident workgroups per CU for the trace kernel (occupancy query).
 int trace_blocks_per_cu(int precision, size_t lds, int var);
 constexpr int kTraceBlock = 256;
+// Per-wave LDS slots of coop_reject (rtw_trace.hip CoopSlots: 64 x u64 + 64 x u32).
+constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;
 
 }  // namespace rtwk

@@ -33,13 +33,22 @@ constexpr double kP3 = 4.04453249742233291160e-21;      // 2 * pio2_3  0x3BB3198
 constexpr double kP4 = 1.69568553207377991399e-31;      // 2 * pio2_3t 0x398B839A252049C1
 constexpr double kSinSignMax = 524288.0;                // 2^19
 
+// Out-of-range arguments (|a| >= 2^19, not produced by the cover scene): libm.
+// Kept out of line so its constants do not occupy registers of the kernel.
+#if defined(__HIPCC__)
+__host__ __device__ __noinline__
+#else
+inline
+#endif
+int sin_sign_libm(double a) {
+  const double s = std::sin(a);
+  return (s > 0) - (s < 0);
+}
+
 // -1, 0 or +1: the sign of sin(a).
 RTW_HD int sin_sign(double a) {
   if (a == 0.0) return 0;  // sin(+-0) = +-0: product == 0, "not < 0"
-  if (!(std::fabs(a) < kSinSignMax)) {
-    const double s = std::sin(a);
-    return (s > 0) - (s < 0);
-  }
+  if (__builtin_expect(!(std::fabs(a) < kSinSignMax), 0)) return sin_sign_libm(a);
   const double k = std::rint(a * kInvPi);
   double r = std::fma(-k, kP1, a);
   r = std::fma(-k, kP2, r);

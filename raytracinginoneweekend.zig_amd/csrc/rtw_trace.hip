@@ -87,17 +87,25 @@ __device__ __forceinline__ V3<R> ld3(const __attribute__((address_space(4))) R* 
 // 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its
 // draws are SplitMix64.next() from there, turned into reals by Zig's
 // Random.float (oracle/rtw_oracle.c tierb_state / ro_sm_f64 / ro_sm_f32).
+// Every draw is exactly one Weyl step: the rare extra words Random.float needs
+// for a tiny value come from the draw's own extension stream
+// SplitMix64.init(state ^ kExt), so draw k of a block sits at state
+// W + (k + 1) * gamma and any lane can evaluate any draw (coop_reject).
 constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
-__device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
-  st += kGamma;
-  uint64_t z = st;
+constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
+__device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
+  st += kGamma;
+  return sm_mix(st);
+}
 __device__ __forceinline__ uint32_t clz64(uint64_t v) { return v ? (uint32_t)__clzll((long long)v) : 64u; }
 
-__device__ __forceinline__ uint32_t f64_long_lz(uint64_t& st) {  // probability 2^-12 per draw
+__device__ __forceinline__ uint32_t f64_long_lz(uint64_t draw_state) {  // probability 2^-12 per draw
+  uint64_t st = draw_state ^ kExt;
   uint32_t lz = 12;
   for (;;) {
     const uint32_t addl = clz64(sm_next(st));
@@ -124,8 +132,9 @@ __device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
   const uint64_t v = sm_next(st);
   uint32_t lz = clz64(v);
   if (__builtin_expect(lz >= 41, 0)) {  // probability 2^-41
-    lz = 41 + clz64(sm_next(st));
-    if (lz == 41 + 64) lz += (uint32_t)__clz((int)((uint32_t)sm_next(st) | 0x7FFu));
+    uint64_t ext = st ^ kExt;
+    lz = 41 + clz64(sm_next(ext));
+    if (lz == 41 + 64) lz += (uint32_t)__clz((int)((uint32_t)sm_next(ext) | 0x7FFu));
   }
   const uint32_t bits = ((126u - lz) << 23) | ((uint32_t)v & ((1u << 23) - 1));
   return __uint_as_float(bits);
@@ -194,6 +203,102 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// ------------------------------------------------- cooperative rejection ----
+// The reference's rejection loops (rand.zig:22-28 randomPointInUnitSphere,
+// rand.zig:30-36 randomPointInUnitDisk) take the FIRST candidate inside the
+// unit ball.  Per lane that is ~1.9 (ball) / ~1.3 (disk) candidates, but a
+// wave waits for its unluckiest lane (~6.9 / ~3.6 wave iterations).  Because
+// candidate q of a D-dim loop whose state is B uses the draws at states
+// B + (D*q + i + 1) * gamma (one Weyl step per draw), the wave can instead
+// deal the candidates of its still-pending lanes to ALL 64 lanes: with m
+// pending lanes each gets c = 2^floor(log2(64/m)) candidates per round,
+// evaluated in parallel; the owner takes the lowest accepted one.  Same
+// candidate order, same result bits, ~3 rounds instead of ~7 iterations.
+// Must be called in wave-converged control flow (every lane of the wave).
+struct CoopSlots {
+  uint64_t st[64];  // pending lane's state B, by rank
+  uint32_t q[64];   // its next candidate index
+};
+constexpr size_t kCoopBytesPerWave = sizeof(CoopSlots);
+static_assert(kCoopBytesPerWave * (kTraceBlock / 64) == kCoopLdsBytes, "rtw_internal.hpp kCoopLdsBytes");
+
+template <typename R, int D>
+__device__ __forceinline__ bool in_unit_ball(const R (&x)[D]) {
+  if constexpr (D == 2)
+    return !(x[0] * x[0] + x[1] * x[1] + (R)0 * (R)0 >= (R)1);  // rand.zig:34: vec3(x, y, 0)
+  else
+    return !(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] >= (R)1);  // rand.zig:26; sqrt(t) >= 1 <=> t >= 1
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename R, int D, bool COOP>
+__device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], CoopSlots* slots, uint32_t lid) {
+  if constexpr (!COOP) {  // the literal per-lane loop (tuning variant 16)
+    if (need) {
+      for (;;) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) x[i] = rrange_m11<R>(st);
+        if (in_unit_ball<R, D>(x)) break;
+      }
+    }
+    return;
+  }
+  bool pending = false;
+  if (need) {  // round 0: every lane its own first candidate
+#pragma unroll
+    for (int i = 0; i < D; ++i) x[i] = rrange_m11<R>(st);
+    pending = !in_unit_ball<R, D>(x);
+  }
+  uint64_t P = __ballot(pending);
+  uint32_t nextq = 0;  // candidates are counted from B = st
+  while (P) {
+    const uint32_t m = (uint32_t)__popcll(P);
+    const uint32_t lc = 31u - (uint32_t)__clz((int)(64u / m));  // c = 2^lc, c*m <= 64
+    const uint32_t r = mbcnt64(P);
+    if (pending) {
+      slots->st[r] = st;
+      slots->q[r] = nextq;
+    }
+    wave_lds_sync();
+    const uint32_t orank = lid >> lc;
+    bool ok = false;
+    R y[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) y[i] = (R)0;
+    if (orank < m) {
+      uint64_t s = slots->st[orank] + (uint64_t)(D * (slots->q[orank] + (lid & ((1u << lc) - 1u)))) * kGamma;
+#pragma unroll
+      for (int i = 0; i < D; ++i) y[i] = rrange_m11<R>(s);
+      ok = in_unit_ball<R, D>(y);
+    }
+    const uint64_t acc = __ballot(ok);
+    wave_lds_sync();  // slots are rewritten next round
+    const uint32_t first = (r << lc) & 63u;  // pending lanes: r*c < 64
+    const uint64_t mine = lc == 6u ? acc : (acc >> first) & ((1ull << (1u << lc)) - 1ull);
+    const uint32_t jj = mine ? (uint32_t)__builtin_ctzll(mine) : 0u;
+    const int src = (int)(first + jj);
+    R z[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) z[i] = __shfl(y[i], src);
+    if (pending) {
+      if (mine) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) x[i] = z[i];
+        st += (uint64_t)(D * (nextq + jj + 1u)) * kGamma;
+        pending = false;
+      } else {
+        nextq += 1u << lc;
+      }
+    }
+    P = __ballot(pending);
+  }
+}
+
 // v / |v| with the three divisions done against RN(1/|v|) (rtw_math.hpp div_rn).
 template <typename R>
 __device__ __forceinline__ V3<R> normalized_rn(V3<R> v) {  // vec.zig:32-39
@@ -204,21 +309,22 @@ __device__ __forceinline__ V3<R> normalized_rn(V3<R> v) {  // vec.zig:32-39
 }
 
 // Camera.getRay (main.zig:91-100) after the u,v jitter (main.zig:390-391).
+// Part 1: the sample's RNG block and the u, v jitter (main.zig:390-391).
 template <typename R>
-__device__ __forceinline__ void start_sample(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L) {
+__device__ __forceinline__ void start_sample_uv(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, R& u, R& v) {
   const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
   const uint32_t y = A.row_begin + L.ly * A.row_stride;  // image row (top-first)
   const uint32_t j = A.H - 1 - y;                        // reference row index
   const uint64_t pixel = (uint64_t)y * A.W + L.px;
   L.rs = A.seed_base + ((((pixel << 24) | (uint64_t)L.s)) << 16) * kGamma;
-  const R u = rtwm::div_rn((R)L.px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
-  const R v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
-  R dx, dy;
-  for (;;) {  // rand.zig:30-36; sqrt(x) >= 1 <=> x >= 1 for correctly rounded sqrt
-    dx = rrange_m11<R>(L.rs);
-    dy = rrange_m11<R>(L.rs);
-    if (!(dx * dx + dy * dy + (R)0 * (R)0 >= (R)1)) break;
-  }
+  u = rtwm::div_rn((R)L.px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
+  v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
+}
+// Part 2, after the lens-disk point (rand.zig:30-36, coop_reject<R, 2>).
+template <typename R>
+__device__ __forceinline__ void start_sample_ray(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, R u, R v, R dx,
+                                                 R dy) {
+  const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
   const V3<R> rd = mk(dx * A.lens_radius, dy * A.lens_radius, (R)0 * A.lens_radius);
   const V3<R> cu = ld3(A.cu), cv = ld3(A.cv), org = ld3(A.origin);
   const V3<R> offset = add(mul(cu, rd.x), mul(cv, rd.y));
@@ -321,14 +427,20 @@ __device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* 
 
 // VAR (tuning variants, selected at launch): bit0 = sphere records from LDS
 // instead of scalar loads; bit1 = unroll the sphere loop by 2; bit2 = ask for
-// 4 waves per SIMD (VGPR budget 128).
+// 4 waves per SIMD (VGPR budget 128); bit3 = 5 waves per SIMD (budget 96);
+// bit4 = per-lane rejection loops instead of coop_reject; bit5 = coop_reject
+// for the lens disk too.
 template <typename R, bool F32, int MODE, int VAR>
-__global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(TraceArgs<R> A) {
+__global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 1)) trace_kernel(TraceArgs<R> A) {
   constexpr bool STATS = MODE == 1;
+  constexpr bool COOP = !(VAR & 16);               // unit-ball point (scatter)
+  constexpr bool COOP_DISK = COOP && (VAR & 32);  // lens-disk point (camera ray)
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const SceneView<R> S = A.sc;
-  // LDS copies of the per-lane lookup tables (winning sphere, its material).
-  R* l_sph = reinterpret_cast<R*>(lds_raw);
+  // LDS: per-wave coop_reject slots, then copies of the per-lane lookup
+  // tables (winning sphere, its material).
+  CoopSlots* slots = reinterpret_cast<CoopSlots*>(lds_raw) + (threadIdx.x >> 6);
+  R* l_sph = reinterpret_cast<R*>(lds_raw + kCoopBytesPerWave * (kTraceBlock / 64));
   R* l_rad = l_sph + 8 * (S.n + 1);
   R* l_mat = l_rad + S.n;
   R* l_tg = l_mat + 8 * S.nm;
@@ -418,16 +530,37 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
     RTW_STAMP(0)
 
     // ---- 2. new samples: per-sample RNG block + camera ray ----
-    if (have_unit && !have_ray) {
-      start_sample<R>(kargs<R>(), L);
-      have_ray = true;
+    {
+      const bool ns = have_unit && !have_ray;
+      if constexpr (COOP_DISK) {
+        if (__any(ns)) {  // wave-uniform: coop_reject runs converged
+          R u = (R)0, v = (R)0, dk[2];
+          if (ns) start_sample_uv<R>(kargs<R>(), L, u, v);
+          coop_reject<R, 2, true>(ns, L.rs, dk, slots, lid);
+          if (ns) {
+            start_sample_ray<R>(kargs<R>(), L, u, v, dk[0], dk[1]);
+            have_ray = true;
+          }
+        }
+      } else if (ns) {
+        R u, v, dk[2];
+        start_sample_uv<R>(kargs<R>(), L, u, v);
+        coop_reject<R, 2, false>(true, L.rs, dk, slots, lid);
+        start_sample_ray<R>(kargs<R>(), L, u, v, dk[0], dk[1]);
+        have_ray = true;
+      }
     }
     RTW_STAMP(1)
 
     // ---- 3. one bounce segment ----
+    // 3a. closest hit (lanes with a live ray); 3b. the unit-ball point for
+    // diffuse/metal lanes (converged); 3c. hit record + scatter.  Only the
+    // winner, its distance and its material cross 3b (register pressure).
+    bool ended = false, shading = false;
+    uint32_t kind = 0;
+    int hit = -1;
+    R tmax = kInf;
     if (have_ray) {
-      bool ended = false;
-      V3<R> col = mk((R)0, (R)0, (R)0);
       if (L.depth == A.max_depth) {  // rayColor depth == 0 (main.zig:105-108)
         ended = true;
       } else {
@@ -438,8 +571,6 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
         const R a = norm2(L.d);
         const R inv_a = (R)1 / a;          // RN(1/a): roots via div_rn
         const R pre_lim = A.pre_k * a;     // "both roots behind" prefilter bound
-        R tmax = kInf;
-        int hit = -1;
         int tg_cur = -1;
         R frac = (R)0;
         const RTW_CONST uint32_t* c_meta = cptr(S.meta);
@@ -561,9 +692,24 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
         RTW_STAMP(2)
 
         if (hit < 0) {  // miss: background (main.zig:109-112)
+          const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
+          L.sx += (double)col.x;
+          L.sy += (double)col.y;
+          L.sz += (double)col.z;
           ended = true;
-          col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
         } else {
+          kind = l_kind[(l_meta[hit] >> 8) & 0xFFFu];
+          shading = true;
+        }
+      }
+    }
+    RTW_STAMP(3)
+    {
+      // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
+      const bool nb = shading && kind <= 2u;
+      R b3[3] = {(R)0, (R)0, (R)0};
+      if (__any(nb)) coop_reject<R, 3, COOP>(nb, L.rs, b3, slots, lid);
+      if (shading) {
           // Hit record of the winner (hittable.zig:118-128, :189-198).
           const R* sp = l_sph + 8 * hit;
           const uint32_t meta = l_meta[hit];
@@ -580,21 +726,11 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
                                    rtwm::div_rn(q.z, rad, inv_r));
           const bool front = dot(outward, L.d) < (R)0;
           const V3<R> normal = front ? outward : mul(outward, (R)-1);
-          const uint32_t mi = (meta >> 8) & 0xFFFu;
-          const uint32_t kind = l_kind[mi];
-          const R* mp = l_mat + 8 * mi;
+          const R* mp = l_mat + 8 * ((meta >> 8) & 0xFFFu);
           // Material.scatter (material.zig:22-29), lanes of one kind together.
           V3<R> ud = L.d;
           if (kind >= 2u) ud = normalized_rn(L.d);  // metal / dielectric
-          V3<R> rs = mk((R)0, (R)0, (R)0);
-          if (kind <= 2u) {  // randomPointInUnitSphere (rand.zig:22-28)
-            for (;;) {
-              rs.x = rrange_m11<R>(L.rs);
-              rs.y = rrange_m11<R>(L.rs);
-              rs.z = rrange_m11<R>(L.rs);
-              if (!(norm2(rs) >= (R)1)) break;
-            }
-          }
+          const V3<R> rs = mk(b3[0], b3[1], b3[2]);
           V3<R> ndir, att;
           bool absorbed = false;
           if (kind <= 1u) {  // Lambertian (material.zig:44-52)
@@ -642,23 +778,19 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 4) ? 4 : 1) trace_kernel(T
             L.d = ndir;
             L.depth++;
           }
-        }
       }
-      RTW_STAMP(3)
-      if (ended) {
-        L.sx += (double)col.x;
-        L.sy += (double)col.y;
-        L.sz += (double)col.z;
-        L.s++;
-        have_ray = false;
-        if (STATS) st_samples++;
-        if (L.s == L.s_end) {  // unit done: publish the chunk sum
-          double* dst = A.partial + ((size_t)L.c * npix + (size_t)L.ly * A.W + L.px) * 3;
-          dst[0] = L.sx;
-          dst[1] = L.sy;
-          dst[2] = L.sz;
-          have_unit = false;
-        }
+    }
+    RTW_STAMP(3)
+    if (ended) {  // (a miss added its colour above; depth limit and absorption add 0)
+      L.s++;
+      have_ray = false;
+      if (STATS) st_samples++;
+      if (L.s == L.s_end) {  // unit done: publish the chunk sum
+        double* dst = A.partial + ((size_t)L.c * npix + (size_t)L.ly * A.W + L.px) * 3;
+        dst[0] = L.sx;
+        dst[1] = L.sy;
+        dst[2] = L.sz;
+        have_unit = false;
       }
     }
   }
@@ -700,24 +832,31 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinalizeArgs F) {
 
 template <typename R, bool F32, int VAR>
 static void launch_var(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
+#ifndef RTW_ISA_QUICK  // (register-pressure experiments: product variants only)
   if (mode == 1)
     hipLaunchKernelGGL((trace_kernel<R, F32, 1, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (mode == 2)
     hipLaunchKernelGGL((trace_kernel<R, F32, 2, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else
+#endif
     hipLaunchKernelGGL((trace_kernel<R, F32, 0, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
 }
 template <typename R, bool F32>
 static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
                                int var) {
-  switch (var & 7) {
+  switch (var) {
+#ifndef RTW_ISA_QUICK
     case 1: launch_var<R, F32, 1>(a, grid, lds, s, mode); break;
-    case 2: launch_var<R, F32, 2>(a, grid, lds, s, mode); break;
-    case 3: launch_var<R, F32, 3>(a, grid, lds, s, mode); break;
     case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
     case 5: launch_var<R, F32, 5>(a, grid, lds, s, mode); break;
-    case 6: launch_var<R, F32, 6>(a, grid, lds, s, mode); break;
-    case 7: launch_var<R, F32, 7>(a, grid, lds, s, mode); break;
+    case 9: launch_var<R, F32, 9>(a, grid, lds, s, mode); break;
+    case 16: launch_var<R, F32, 16>(a, grid, lds, s, mode); break;
+    case 24: launch_var<R, F32, 24>(a, grid, lds, s, mode); break;
+    case 32: launch_var<R, F32, 32>(a, grid, lds, s, mode); break;
+    case 36: launch_var<R, F32, 36>(a, grid, lds, s, mode); break;
+    case 20: launch_var<R, F32, 20>(a, grid, lds, s, mode); break;
+#endif
+    case 8: launch_var<R, F32, 8>(a, grid, lds, s, mode); break;
     default: launch_var<R, F32, 0>(a, grid, lds, s, mode); break;
   }
   return hipGetLastError();
@@ -746,11 +885,13 @@ static int occ(size_t lds) {
 }
 int trace_blocks_per_cu(int precision, size_t lds, int var) {
   int nb = 0;
-  switch (var & 7) {
+  switch (var) {
 #define RTW_OCC_CASE(v) \
   case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
-    RTW_OCC_CASE(0) RTW_OCC_CASE(1) RTW_OCC_CASE(2) RTW_OCC_CASE(3)
-    RTW_OCC_CASE(4) RTW_OCC_CASE(5) RTW_OCC_CASE(6) RTW_OCC_CASE(7)
+#ifndef RTW_ISA_QUICK
+    RTW_OCC_CASE(1) RTW_OCC_CASE(4) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20)
+#endif
+    RTW_OCC_CASE(0) RTW_OCC_CASE(8)
 #undef RTW_OCC_CASE
   }
   return nb > 0 ? nb : 1;
