@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "rtw_hip.h"
+#include "rtw_cull.hpp"
 #include "rtw_internal.hpp"
 
 namespace {
@@ -75,7 +76,7 @@ int blocks_per_cu(int dev, int prec, size_t lds, int var) {
 int kernel_variant(uint32_t precision) {
   const char* v = getenv("RTW_VARIANT");
   if (v && *v) return atoi(v);
-  return precision == RTW_PRECISION_F32 ? 8 : 4;
+  return precision == RTW_PRECISION_F32 ? 8 : 4;  // (both with the narrow-sphere pretest)
 }
 
 }  // namespace
@@ -205,6 +206,36 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
     tg32[4 * g + 1] = f1;
     tg32[4 * g + 2] = 1.0f / (f1 - f0);
   }
+  // Pretest records (rtw_cull.hpp) over the narrow spheres in table order.
+  const uint32_t n_sn = g_end[1] - g_end[0], nn = n_sn + (n - g_end[2]);
+  const uint32_t nn_pad = (nn + 31u) & ~31u;
+  std::vector<float> cull((size_t)8 * nn_pad + 16, 0.0f);  // + one padding pair (prefetch)
+  std::vector<uint32_t> cull_tg(nn_pad / 2 + 1, 0u);
+  double cmax_c = 0.0, cmax_d = 0.0;
+  for (uint32_t j = 0; j < nn; ++j) {
+    const uint32_t pos = j < n_sn ? g_end[0] + j : g_end[2] + (j - n_sn);
+    const double* r = &sph64[8 * pos];
+    float* q = &cull[(size_t)16 * (j / 2) + (j & 1)];
+    for (int k = 0; k < 3; ++k) {
+      q[2 * k] = (float)r[k];
+      q[2 * (3 + k)] = -(float)r[3 + k];
+      cmax_c = std::max(cmax_c, std::fabs(r[k]));
+      cmax_d = std::max(cmax_d, std::fabs(r[3 + k]));
+    }
+    const float rf = (float)rad64[pos];
+    q[12] = -(rf * rf);
+    q[14] = std::nextafter((float)(2.0 * r[6] + 1.0), INFINITY);
+    const uint32_t g = (meta[pos] & rtwk::kMoving) ? (meta[pos] >> 2) & 63u : 0u;
+    cull_tg[j / 2] |= g << (8 * (j & 1));
+  }
+  for (uint32_t j = nn; j < nn_pad; ++j)  // padding: same time group as its partner
+    if (j & 1) cull_tg[j / 2] |= (cull_tg[j / 2] & 0xFFu) << 8;
+  for (uint32_t j = 0; j + 1 < nn; j += 2) {  // static half of a mixed pair: partner's group
+    const bool m0 = j >= n_sn, m1 = j + 1 >= n_sn;
+    if (!m0 && m1) cull_tg[j / 2] = (cull_tg[j / 2] & 0xFF00u) | (cull_tg[j / 2] >> 8);
+  }
+  const float cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
+  const uint32_t cull_on = (nn > 0 && cmax <= rtwc::kCmaxLimit) ? 1u : 0u;
   // One device allocation, 256-B aligned sub-buffers.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   size_t off = 0;
@@ -218,6 +249,7 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   const size_t o_sph32 = place(sph32.size() * 4), o_rad32 = place(rad32.size() * 4);
   const size_t o_mat32 = place(mat32.size() * 4), o_tg32 = place(tg32.size() * 4);
   const size_t o_meta = place(meta.size() * 4), o_kind = place(kind.size() * 4), o_perm = place(perm.size() * 4);
+  const size_t o_cull = place(cull.size() * 4), o_cull_tg = place(cull_tg.size() * 4);
   const size_t total = off;
   std::vector<unsigned char> host(total, 0);
   auto cp = [&](size_t o, const void* p, size_t bytes) {
@@ -234,6 +266,8 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   cp(o_meta, meta.data(), meta.size() * 4);
   cp(o_kind, kind.data(), kind.size() * 4);
   cp(o_perm, perm.data(), perm.size() * 4);
+  cp(o_cull, cull.data(), cull.size() * 4);
+  cp(o_cull_tg, cull_tg.data(), cull_tg.size() * 4);
 
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -257,9 +291,11 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   auto F = [&](size_t o) { return reinterpret_cast<const float*>(b + o); };
   auto U = [&](size_t o) { return reinterpret_cast<const uint32_t*>(b + o); };
   sc->v64 = {D(o_sph64), D(o_rad64), U(o_meta), D(o_mat64), U(o_kind), D(o_tg64), D(o_sph64), D(o_tg64), U(o_perm),
-             n, nm, ng, g_end[0], g_end[1], g_end[2]};
+             F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
+             cmax};
   sc->v32 = {F(o_sph32), F(o_rad32), U(o_meta), F(o_mat32), U(o_kind), F(o_tg32), D(o_sph64), D(o_tg64), U(o_perm),
-             n, nm, ng, g_end[0], g_end[1], g_end[2]};
+             F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
+             cmax};
   *out = sc;
   return RTW_OK;
 }
@@ -477,12 +513,12 @@ int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, mode);
   if (r != RTW_OK) return r;
   HIP_TRY(hipDeviceSynchronize());
-  unsigned long long st[16] = {0};
+  unsigned long long st[32] = {0};
   const WsLayout L = ws_layout(p);
   HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
   if (mode == 1 && getenv("RTW_COUNTS_VERBOSE")) {
     fprintf(stderr, "[rtw counts] samples %llu segments %llu skipped %llu cand_wave_iters %llu cand_lanes %llu "
-            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
+            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[16]);
   }
   if (mode == 2) {
     const char* names[6] = {"refill", "start_sample", "sphere_loop", "shade", "tail", "loop_top"};

@@ -1,0 +1,70 @@
+// rtw_cull.hpp — conservative f32 pretest for the closest-hit loop.
+//
+// Sphere.hit / MovingSphere.hit (hittable.zig:95-101, :165-171) reject a
+// sphere when disc = half_b^2 - a*c < 0; ~97 % of (ray, sphere) tests end
+// there.  The kernel first evaluates disc for two spheres at once in packed
+// f32 (v_pk_fma_f32) and adds a margin M larger than the total error of that
+// estimate; x = disc_f32 + M < 0 PROVES that the exact discriminant (f64, or
+// f32 in precision 1) is negative, so the exact test of that sphere can be
+// skipped without changing any result.  Survivors get the exact test.
+//
+// Error budget (P = |o - c|, D = |d|, e = absolute error of each component of
+// o - c as computed here, u = 2^-24; first order, Cauchy-Schwarz |hb| <= PD):
+//   |disc_f32 - disc| <= D^2 [4 sqrt(3) P e + 22 u P^2 + 5 u r^2 + 7 e^2]
+//                     <= D^2 [(3.5 e + 22 u)(P^2 + 1) + 5 u r^2 + 7 e^2]
+// and e <= 4u (|o|_inf + Cmax) with Cmax = max |c0|_inf + |c1 - c0|_inf over
+// the narrow spheres.  The kernel uses M = alpha * (cc + rho) with
+// alpha = a (16 e' + 100 u), e' = 8u (|o|_inf + Cmax) (a 4x-8x safety
+// factor on every term), cc + rho = P^2 + r^2 + 1 (rho = 2 r^2 + 1).  Lanes
+// with |o|_inf > 2^20 or a outside [2^-40, 2^40] (or non-finite values) do
+// not use the pretest; scenes with Cmax > 2^20 do not either.
+// tests/test_cull_host.py checks the bound on adversarial near-grazing cases.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define RTWC_HD __host__ __device__ __forceinline__
+#else
+#define RTWC_HD inline
+#endif
+
+namespace rtwc {
+
+constexpr float kU = 0x1p-24f;
+constexpr float kOriginMax = 0x1p20f;  // |o|_inf limit of a lane that uses the pretest
+constexpr float kCmaxLimit = 0x1p20f;  // scene limit
+
+struct LaneCull {
+  float alpha;  // margin scale
+  bool ok;      // lane may use the pretest
+};
+
+RTWC_HD LaneCull lane_cull(float ox, float oy, float oz, float a, float cmax) {
+  const float om = std::fmax(std::fabs(ox), std::fmax(std::fabs(oy), std::fabs(oz)));
+  const bool ok = (om <= kOriginMax) & (a >= 0x1p-40f) & (a <= 0x1p40f);
+  const float e = (om + cmax) * (8.0f * kU);
+  return {a * std::fma(16.0f, e, 100.0f * kU), ok};
+}
+
+// One sphere of a pretest record: c = f32(c0), ndc = -f32(c1 - c0),
+// nr2 = -f32(r)^2, rho = 2 r^2 + 1 rounded up.  frac = f32 estimate of
+// (time - t0) / (t1 - t0) (any finite value for a static sphere, ndc = 0).
+// Returns x: x < 0 proves disc < 0.  Operation order = the kernel's packed
+// code (rtw_trace.hip cull_pair), so host and device give the same bits.
+RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz, float a, float alpha, float frac,
+                     float cx, float cy, float cz, float ndcx, float ndcy, float ndcz, float nr2, float rho,
+                     bool moving) {
+  float ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+  if (moving) {
+    ocx = std::fma(ndcx, frac, ocx);
+    ocy = std::fma(ndcy, frac, ocy);
+    ocz = std::fma(ndcz, frac, ocz);
+  }
+  const float hb = std::fma(ocz, dz, std::fma(ocy, dy, ocx * dx));
+  const float cc = std::fma(ocz, ocz, std::fma(ocy, ocy, std::fma(ocx, ocx, nr2)));
+  const float disc = std::fma(-a, cc, hb * hb);
+  return std::fma(alpha, cc + rho, disc);
+}
+
+}  // namespace rtwc

@@ -14,6 +14,9 @@
 //   tg_R   : ng x 4 R   {t0, t1, RN(1/(t1-t0)), 0} per distinct MovingSphere (time0, time1)
 //   wide_d : n x 8 f64  f64 copy of sph (f32 mode solves wide spheres in f64)
 //   tg_d   : ng x 4 f64
+//   cull   : nn_pad/2 x 16 f32  pretest pairs over the narrow spheres in table
+//            order (static narrow, then moving narrow; rtw_cull.hpp)
+//   cull_tg: nn_pad/2 x u32     time groups of each pair
 // R = double (precision 0) and float (precision 1) copies are both kept.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -39,8 +42,14 @@ struct SceneView {
   const double* wide_d;
   const double* tg_d;
   const uint32_t* perm;
+  const float* cull;     // pretest records, nn_pad / 2 pairs x 16 f32 (rtw_trace.hip cull_pair)
+  const uint32_t* cull_tg;  // per pair: time group of sphere 2p | (of 2p+1) << 8
+  const float* tg_f;     // f32 time groups (t0, t1, 1/(t1-t0), 0) for the pretest
   uint32_t n, nm, ng;
   uint32_t g_static_wide, g_static, g_moving_wide;  // group ends; the moving group ends at n
+  uint32_t nn, nn_pad, n_sn;  // narrow spheres (static narrow first), padded to 32; static narrow count
+  uint32_t cull_on;           // pretest usable for this scene (rtw_cull.hpp limits)
+  float cull_cmax;            // max |c0|_inf + |c1 - c0|_inf over narrow spheres (rounded up)
 };
 
 template <typename R>

@@ -26,6 +26,7 @@
 // The oracle's tierb_core.h is the written contract this file implements.
 #include <hip/hip_runtime.h>
 
+#include "rtw_cull.hpp"
 #include "rtw_internal.hpp"
 #include "rtw_math.hpp"
 
@@ -180,6 +181,38 @@ __device__ __forceinline__ const RTW_CONST T* opaque(const RTW_CONST T* p) {
 template <typename R>
 __device__ __forceinline__ const RTW_CONST TraceArgs<R>* kargs() {
   return (const RTW_CONST TraceArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
+// ---------------------------------------------------- packed-f32 pretest --
+// Two spheres per v_pk_fma_f32 (rtw_cull.hpp: the bound and the scalar
+// statement of the same operations).  Record of pair p (64 B, scalar-loaded):
+// {c.x, c.y, c.z, ndc.x, ndc.y, ndc.z, nr2, rho}, each as {sphere 2p, 2p+1}.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+struct PairRec {
+  f2 v[8];
+};
+__device__ __forceinline__ PairRec ld_pair(const __attribute__((address_space(4))) f2* t, uint32_t p) {
+  PairRec r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = t[8 * p + i];
+  return r;
+}
+template <bool MOVING>
+__device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, f2 na, f2 alpha,
+                                        f2 frac) {
+  const f2* P = R_.v;
+  f2 ocx = ox - P[0], ocy = oy - P[1], ocz = oz - P[2];
+  if constexpr (MOVING) {
+    ocx = pfma(P[3], frac, ocx);
+    ocy = pfma(P[4], frac, ocy);
+    ocz = pfma(P[5], frac, ocz);
+  }
+  const f2 hb = pfma(ocz, dz, pfma(ocy, dy, ocx * dx));
+  const f2 cc = pfma(ocz, ocz, pfma(ocy, ocy, pfma(ocx, ocx, P[6])));
+  const f2 disc = pfma(na, cc, hb * hb);
+  return pfma(alpha, cc + P[7], disc);
 }
 
 template <typename R>
@@ -429,10 +462,12 @@ __device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* 
 // instead of scalar loads; bit1 = unroll the sphere loop by 2; bit2 = ask for
 // 4 waves per SIMD (VGPR budget 128); bit3 = 5 waves per SIMD (budget 96);
 // bit4 = per-lane rejection loops instead of coop_reject; bit5 = coop_reject
-// for the lens disk too.
+// for the lens disk too; bit6 = no narrow-sphere pretest (every lane tests
+// every sphere exactly).
 template <typename R, bool F32, int MODE, int VAR>
 __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 1)) trace_kernel(TraceArgs<R> A) {
   constexpr bool STATS = MODE == 1;
+  constexpr bool CULL = !(VAR & 64);                // packed-f32 pretest for narrow spheres
   constexpr bool COOP = !(VAR & 16);               // unit-ball point (scatter)
   constexpr bool COOP_DISK = COOP && (VAR & 32);  // lens-disk point (camera ray)
   extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -472,7 +507,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   bool done = false;       // queue exhausted for this lane
   uint32_t qnext = 0, qend = 0;  // wave-uniform batch [qnext, qend)
   unsigned long long st_samples = 0, st_segments = 0, st_skipped = 0;
-  unsigned long long st_candwave = 0, st_candlane = 0, st_disc = 0, st_iters = 0, st_wave_iters = 0;
+  unsigned long long st_candwave = 0, st_candlane = 0, st_disc = 0, st_wave_iters = 0;
+  unsigned long long st_cull_lanes = 0, st_cull_iters = 0;
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
   uint64_t t_last = 0;
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last)::"memory");
@@ -652,8 +688,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           wide_range(S.g_static, S.g_moving_wide);
         }
         // static spheres: records stream one step ahead (padding record at the end)
-        {
-          const uint32_t b = F32 ? S.g_static_wide : 0u, e = S.g_static;
+        auto static_range = [&](uint32_t b, uint32_t e) {
           if (b < e) {
             Rec<R> cur = rec_at(b);
 #pragma unroll(((VAR & 2) ? 2 : 1))
@@ -663,10 +698,9 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
               cur = nxt;
             }
           }
-        }
+        };
         // moving spheres: centre(t) = c0 + (c1 - c0) * frac (hittable.zig:219-221)
-        {
-          const uint32_t b = F32 ? S.g_moving_wide : S.g_static, e = S.n;
+        auto moving_range = [&](uint32_t b, uint32_t e) {
           if (b < e) {
             Rec<R> cur = rec_at(b);
 #pragma unroll(((VAR & 2) ? 2 : 1))
@@ -680,6 +714,105 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
               test(k, cur.meta, cur.c[0] + cur.dc[0] * frac, cur.c[1] + cur.dc[1] * frac, cur.c[2] + cur.dc[2] * frac,
                    cur.r2);
               cur = nxt;
+            }
+          }
+        };
+        if (!CULL || !S.cull_on) {
+          static_range(F32 ? S.g_static_wide : 0u, S.g_static);
+          moving_range(F32 ? S.g_moving_wide : S.g_static, S.n);
+        } else {
+          if constexpr (!F32) {  // wide spheres: exact, wave-uniform
+            static_range(0u, S.g_static_wide);
+            moving_range(S.g_static, S.g_moving_wide);
+          }
+          // Narrow spheres: the packed-f32 pretest (rtw_cull.hpp) proves
+          // disc < 0 for most (lane, sphere) pairs; each lane then runs the
+          // exact test only on the spheres it could not rule out.
+          const float af = (float)a;
+          const rtwc::LaneCull lc = rtwc::lane_cull((float)L.o.x, (float)L.o.y, (float)L.o.z, af, S.cull_cmax);
+          const f2 ox = bc((float)L.o.x), oy = bc((float)L.o.y), oz = bc((float)L.o.z);
+          const f2 dx = bc((float)L.d.x), dy = bc((float)L.d.y), dz = bc((float)L.d.z);
+          const f2 na = bc(-af), alpha = bc(lc.alpha);
+          const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(S.cull));
+          const RTW_CONST uint32_t* ctg = cptr(S.cull_tg);
+          const RTW_CONST float* ctf = cptr(S.tg_f);
+          const float tf = (float)L.time;
+          const uint32_t np_static = S.n_sn >> 1;  // pairs with two static spheres
+          int fr_g = -1;  // phase B: time group of fr_v
+          R fr_v = (R)0;
+          for (uint32_t base = 0; base < S.nn; base += 64) {
+            uint32_t sk[2] = {0u, 0u};  // bit 31-r of sk[h]: sphere base+32h+r proven to miss
+            uint32_t tgp_cur = ~0u;
+            f2 fr2 = bc(0.0f);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t p0 = (base >> 1) + 16u * h, p1 = min(p0 + 16u, (S.nn + 1u) >> 1);
+              // pair records stream one step ahead (the table has a padding pair)
+              if (p0 < p1) {
+                PairRec cur = ld_pair(ct, p0);
+                uint32_t tgp_nxt = ctg[p0];
+                for (uint32_t p = p0; p < p1; ++p) {
+                  const PairRec nxt = ld_pair(ct, p + 1);
+                  const uint32_t tgp = tgp_nxt;
+                  tgp_nxt = ctg[p + 1];
+                  f2 x;
+                  if (p < np_static) {
+                    x = cull_pair<false>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                  } else {
+                    if (tgp != tgp_cur) {  // wave-uniform
+                      tgp_cur = tgp;
+                      const uint32_t g0 = tgp & 0xFFu, g1 = tgp >> 8;
+                      fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
+                    }
+                    x = cull_pair<true>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                  }
+                  sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.x), 31);
+                  sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.y), 31);
+                  cur = nxt;
+                }
+              }
+              // fewer than 16 pairs: move sphere r of the chunk to bit 31 - r
+              const uint32_t cnt = p1 > p0 ? 2u * (p1 - p0) : 0u;
+              sk[h] = cnt == 0u ? 0u : (cnt == 32u ? sk[h] : sk[h] << (32u - cnt));
+            }
+            const uint32_t rem = S.nn - base;  // real spheres in this block
+            const uint32_t v0 = rem >= 32u ? ~0u : ~(~0u >> rem);
+            const uint32_t v1 = rem >= 64u ? ~0u : (rem <= 32u ? 0u : ~(~0u >> (rem - 32u)));
+            uint32_t m0 = v0, m1 = v1;
+            if (lc.ok) {
+              m0 &= ~sk[0];
+              m1 &= ~sk[1];
+            }
+            if constexpr (STATS) st_cull_lanes += __popc(m0) + __popc(m1);
+            while (m0 | m1) {  // per lane: the exact test on the survivors
+              if constexpr (STATS) {
+                if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_cull_iters++;
+              }
+              uint32_t r;
+              if (m0) {
+                r = __clz(m0);
+                m0 &= ~(0x80000000u >> r);
+              } else {
+                r = __clz(m1);
+                m1 &= ~(0x80000000u >> r);
+                r += 32u;
+              }
+              const uint32_t j = base + r;
+              const uint32_t k = j < S.n_sn ? S.g_static_wide + j : S.g_moving_wide + (j - S.n_sn);
+              const R* sp = l_sph + 8 * k;
+              const uint32_t meta = l_meta[k];
+              R cx = sp[0], cy = sp[1], cz = sp[2];
+              if (meta & kMoving) {
+                const int g = (int)((meta >> 2) & 63u);
+                if (g != fr_g) {  // per lane: usually once per segment
+                  fr_g = g;
+                  fr_v = rtwm::div_rn(L.time - l_tg[4 * g], l_tg[4 * g + 1] - l_tg[4 * g], l_tg[4 * g + 2]);
+                }
+                cx = cx + sp[3] * fr_v;
+                cy = cy + sp[4] * fr_v;
+                cz = cz + sp[5] * fr_v;
+              }
+              test(k, meta, cx, cy, cz, sp[6]);
             }
           }
         }
@@ -802,6 +935,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     atomicAdd(A.stats + 4, st_candlane);
     atomicAdd(A.stats + 5, st_disc);
     atomicAdd(A.stats + 6, st_wave_iters);
+    atomicAdd(A.stats + 7, st_cull_lanes);
+    atomicAdd(A.stats + 16, st_cull_iters);
   }
   if constexpr (MODE == 2) {
     RTW_STAMP(4)
@@ -847,7 +982,6 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
   switch (var) {
 #ifndef RTW_ISA_QUICK
     case 1: launch_var<R, F32, 1>(a, grid, lds, s, mode); break;
-    case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
     case 5: launch_var<R, F32, 5>(a, grid, lds, s, mode); break;
     case 9: launch_var<R, F32, 9>(a, grid, lds, s, mode); break;
     case 16: launch_var<R, F32, 16>(a, grid, lds, s, mode); break;
@@ -855,7 +989,10 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 32: launch_var<R, F32, 32>(a, grid, lds, s, mode); break;
     case 36: launch_var<R, F32, 36>(a, grid, lds, s, mode); break;
     case 20: launch_var<R, F32, 20>(a, grid, lds, s, mode); break;
+    case 68: launch_var<R, F32, 68>(a, grid, lds, s, mode); break;
+    case 72: launch_var<R, F32, 72>(a, grid, lds, s, mode); break;
 #endif
+    case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
     case 8: launch_var<R, F32, 8>(a, grid, lds, s, mode); break;
     default: launch_var<R, F32, 0>(a, grid, lds, s, mode); break;
   }
@@ -889,9 +1026,9 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #define RTW_OCC_CASE(v) \
   case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
 #ifndef RTW_ISA_QUICK
-    RTW_OCC_CASE(1) RTW_OCC_CASE(4) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20)
+    RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(8)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8)
 #undef RTW_OCC_CASE
   }
   return nb > 0 ? nb : 1;
