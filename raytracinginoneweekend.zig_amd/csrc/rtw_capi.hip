@@ -211,7 +211,7 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   const uint32_t nn_pad = (nn + 31u) & ~31u;
   std::vector<float> cull((size_t)8 * nn_pad + 16, 0.0f);  // + one padding pair (prefetch)
   std::vector<uint32_t> cull_tg(nn_pad / 2 + 1, 0u);
-  double cmax_c = 0.0, cmax_d = 0.0;
+  double cmax_c = 0.0, cmax_d = 0.0, rho_max = 1.0;
   for (uint32_t j = 0; j < nn; ++j) {
     const uint32_t pos = j < n_sn ? g_end[0] + j : g_end[2] + (j - n_sn);
     const double* r = &sph64[8 * pos];
@@ -224,7 +224,7 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
     }
     const float rf = (float)rad64[pos];
     q[12] = -(rf * rf);
-    q[14] = std::nextafter((float)(2.0 * r[6] + 1.0), INFINITY);
+    rho_max = std::max(rho_max, 2.0 * r[6] + 1.0);
     const uint32_t g = (meta[pos] & rtwk::kMoving) ? (meta[pos] >> 2) & 63u : 0u;
     cull_tg[j / 2] |= g << (8 * (j & 1));
   }
@@ -235,6 +235,7 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
     if (!m0 && m1) cull_tg[j / 2] = (cull_tg[j / 2] & 0xFF00u) | (cull_tg[j / 2] >> 8);
   }
   const float cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
+  const float rho = std::nextafter((float)rho_max, INFINITY);
   const uint32_t cull_on = (nn > 0 && cmax <= rtwc::kCmaxLimit) ? 1u : 0u;
   // One device allocation, 256-B aligned sub-buffers.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -292,10 +293,10 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   auto U = [&](size_t o) { return reinterpret_cast<const uint32_t*>(b + o); };
   sc->v64 = {D(o_sph64), D(o_rad64), U(o_meta), D(o_mat64), U(o_kind), D(o_tg64), D(o_sph64), D(o_tg64), U(o_perm),
              F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
-             cmax};
+             cmax, rho};
   sc->v32 = {F(o_sph32), F(o_rad32), U(o_meta), F(o_mat32), U(o_kind), F(o_tg32), D(o_sph64), D(o_tg64), U(o_perm),
              F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
-             cmax};
+             cmax, rho};
   *out = sc;
   return RTW_OK;
 }
@@ -518,15 +519,16 @@ int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
   if (mode == 1 && getenv("RTW_COUNTS_VERBOSE")) {
     fprintf(stderr, "[rtw counts] samples %llu segments %llu skipped %llu cand_wave_iters %llu cand_lanes %llu "
-            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[16]);
+            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
   }
   if (mode == 2) {
-    const char* names[6] = {"refill", "start_sample", "sphere_loop", "shade", "tail", "loop_top"};
+    const char* names[10] = {"refill",  "start_sample", "wide+pretest", "hit+kind",    "tail",
+                             "loop_top", "exact_survivors", "coop_ball", "hitrec+scatter", "-"};
     unsigned long long tot = 0;
-    for (int i = 0; i < 6; ++i) tot += st[8 + i];
-    for (int i = 0; i < 6; ++i)
-      fprintf(stderr, "[rtw phase] %-13s %6.2f%%  (%llu wave-cycles)\n", names[i], tot ? 100.0 * st[8 + i] / tot : 0.0,
-              st[8 + i]);
+    for (int i = 0; i < 10; ++i) tot += st[16 + i];
+    for (int i = 0; i < 9; ++i)
+      fprintf(stderr, "[rtw phase] %-15s %6.2f%%  (%llu wave-cycles)\n", names[i], tot ? 100.0 * st[16 + i] / tot : 0.0,
+              st[16 + i]);
   }
   counts_out[0] = st[0];
   counts_out[1] = st[1];

@@ -15,7 +15,10 @@
 // and e <= 4u (|o|_inf + Cmax) with Cmax = max |c0|_inf + |c1 - c0|_inf over
 // the narrow spheres.  The kernel uses M = alpha * (cc + rho) with
 // alpha = a (16 e' + 100 u), e' = 8u (|o|_inf + Cmax) (a 4x-8x safety
-// factor on every term), cc + rho = P^2 + r^2 + 1 (rho = 2 r^2 + 1).  Lanes
+// factor on every term), cc + rho = P^2 + r^2 + 1 (rho = 2 r^2 + 1).  The
+// kernel uses rho_max (over the scene's narrow spheres) for every sphere, so
+// x = hb^2 + alpha rho_max - (a - alpha) cc needs two packed ops past hb, cc,
+// the same as disc alone.  Lanes
 // with |o|_inf > 2^20 or a outside [2^-40, 2^40] (or non-finite values) do
 // not use the pretest; scenes with Cmax > 2^20 do not either.
 // tests/test_cull_host.py checks the bound on adversarial near-grazing cases.
@@ -47,14 +50,19 @@ RTWC_HD LaneCull lane_cull(float ox, float oy, float oz, float a, float cmax) {
   return {a * std::fma(16.0f, e, 100.0f * kU), ok};
 }
 
+// Per-lane constants of the pretest: na = -(a - alpha), k = alpha * rho_max.
+struct LaneConst {
+  float na, k;
+};
+RTWC_HD LaneConst lane_const(float a, float alpha, float rho_max) { return {-(a - alpha), alpha * rho_max}; }
+
 // One sphere of a pretest record: c = f32(c0), ndc = -f32(c1 - c0),
-// nr2 = -f32(r)^2, rho = 2 r^2 + 1 rounded up.  frac = f32 estimate of
-// (time - t0) / (t1 - t0) (any finite value for a static sphere, ndc = 0).
-// Returns x: x < 0 proves disc < 0.  Operation order = the kernel's packed
-// code (rtw_trace.hip cull_pair), so host and device give the same bits.
-RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz, float a, float alpha, float frac,
-                     float cx, float cy, float cz, float ndcx, float ndcy, float ndcz, float nr2, float rho,
-                     bool moving) {
+// nr2 = -f32(r)^2.  frac = f32 estimate of (time - t0) / (t1 - t0) (any
+// finite value for a static sphere, ndc = 0).  Returns x: x < 0 proves
+// disc < 0.  Operation order = the kernel's packed code (rtw_trace.hip
+// cull_pair), so host and device give the same bits.
+RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz, LaneConst lk, float frac, float cx,
+                     float cy, float cz, float ndcx, float ndcy, float ndcz, float nr2, bool moving) {
   float ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
   if (moving) {
     ocx = std::fma(ndcx, frac, ocx);
@@ -63,8 +71,7 @@ RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz,
   }
   const float hb = std::fma(ocz, dz, std::fma(ocy, dy, ocx * dx));
   const float cc = std::fma(ocz, ocz, std::fma(ocy, ocy, std::fma(ocx, ocx, nr2)));
-  const float disc = std::fma(-a, cc, hb * hb);
-  return std::fma(alpha, cc + rho, disc);
+  return std::fma(lk.na, cc, std::fma(hb, hb, lk.k));
 }
 
 }  // namespace rtwc

@@ -50,6 +50,7 @@ struct SceneView {
   uint32_t nn, nn_pad, n_sn;  // narrow spheres (static narrow first), padded to 32; static narrow count
   uint32_t cull_on;           // pretest usable for this scene (rtw_cull.hpp limits)
   float cull_cmax;            // max |c0|_inf + |c1 - c0|_inf over narrow spheres (rounded up)
+  float cull_rho;             // max 2 r^2 + 1 over narrow spheres (rounded up)
 };
 
 template <typename R>

@@ -186,7 +186,7 @@ __device__ __forceinline__ const RTW_CONST TraceArgs<R>* kargs() {
 // ---------------------------------------------------- packed-f32 pretest --
 // Two spheres per v_pk_fma_f32 (rtw_cull.hpp: the bound and the scalar
 // statement of the same operations).  Record of pair p (64 B, scalar-loaded):
-// {c.x, c.y, c.z, ndc.x, ndc.y, ndc.z, nr2, rho}, each as {sphere 2p, 2p+1}.
+// {c.x, c.y, c.z, ndc.x, ndc.y, ndc.z, nr2, unused}, each as {sphere 2p, 2p+1}.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -200,7 +200,7 @@ __device__ __forceinline__ PairRec ld_pair(const __attribute__((address_space(4)
   return r;
 }
 template <bool MOVING>
-__device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, f2 na, f2 alpha,
+__device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, f2 na, f2 k,
                                         f2 frac) {
   const f2* P = R_.v;
   f2 ocx = ox - P[0], ocy = oy - P[1], ocz = oz - P[2];
@@ -211,8 +211,7 @@ __device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, 
   }
   const f2 hb = pfma(ocz, dz, pfma(ocy, dy, ocx * dx));
   const f2 cc = pfma(ocz, ocz, pfma(ocy, ocy, pfma(ocx, ocx, P[6])));
-  const f2 disc = pfma(na, cc, hb * hb);
-  return pfma(alpha, cc + P[7], disc);
+  return pfma(na, cc, pfma(hb, hb, k));
 }
 
 template <typename R>
@@ -509,7 +508,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   unsigned long long st_samples = 0, st_segments = 0, st_skipped = 0;
   unsigned long long st_candwave = 0, st_candlane = 0, st_disc = 0, st_wave_iters = 0;
   unsigned long long st_cull_lanes = 0, st_cull_iters = 0;
-  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_last = 0;
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last)::"memory");
 
@@ -732,7 +731,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           const rtwc::LaneCull lc = rtwc::lane_cull((float)L.o.x, (float)L.o.y, (float)L.o.z, af, S.cull_cmax);
           const f2 ox = bc((float)L.o.x), oy = bc((float)L.o.y), oz = bc((float)L.o.z);
           const f2 dx = bc((float)L.d.x), dy = bc((float)L.d.y), dz = bc((float)L.d.z);
-          const f2 na = bc(-af), alpha = bc(lc.alpha);
+          const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, S.cull_rho);
+          const f2 na = bc(lk.na), alpha = bc(lk.k);
           const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(S.cull));
           const RTW_CONST uint32_t* ctg = cptr(S.cull_tg);
           const RTW_CONST float* ctf = cptr(S.tg_f);
@@ -784,6 +784,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
               m1 &= ~sk[1];
             }
             if constexpr (STATS) st_cull_lanes += __popc(m0) + __popc(m1);
+            RTW_STAMP(2)
             while (m0 | m1) {  // per lane: the exact test on the survivors
               if constexpr (STATS) {
                 if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_cull_iters++;
@@ -814,6 +815,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
               }
               test(k, meta, cx, cy, cz, sp[6]);
             }
+            RTW_STAMP(6)
           }
         }
         // A NaN anywhere makes the reference's acceptance order-dependent:
@@ -842,6 +844,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       const bool nb = shading && kind <= 2u;
       R b3[3] = {(R)0, (R)0, (R)0};
       if (__any(nb)) coop_reject<R, 3, COOP>(nb, L.rs, b3, slots, lid);
+      RTW_STAMP(7)
       if (shading) {
           // Hit record of the winner (hittable.zig:118-128, :189-198).
           const R* sp = l_sph + 8 * hit;
@@ -861,13 +864,15 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           const V3<R> normal = front ? outward : mul(outward, (R)-1);
           const R* mp = l_mat + 8 * ((meta >> 8) & 0xFFFu);
           // Material.scatter (material.zig:22-29), lanes of one kind together.
-          V3<R> ud = L.d;
-          if (kind >= 2u) ud = normalized_rn(L.d);  // metal / dielectric
+          // One normalisation per lane: the unit-ball point (Lambertian) or the
+          // ray direction (Metal, Dielectric).
           const V3<R> rs = mk(b3[0], b3[1], b3[2]);
+          const V3<R> nv = normalized_rn(kind <= 1u ? rs : L.d);
+          const V3<R> ud = nv;
           V3<R> ndir, att;
           bool absorbed = false;
           if (kind <= 1u) {  // Lambertian (material.zig:44-52)
-            ndir = add(normal, normalized_rn(rs));
+            ndir = add(normal, nv);
             if (fabs(ndir.x) < (R)1e-8 && fabs(ndir.y) < (R)1e-8 && fabs(ndir.z) < (R)1e-8) ndir = normal;
             att = ld3(mp);
             // CheckerTexture.value (texture.zig:79-82): only the sign matters.
@@ -913,7 +918,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           }
       }
     }
-    RTW_STAMP(3)
+    RTW_STAMP(8)
     if (ended) {  // (a miss added its colour above; depth limit and absorption add 0)
       L.s++;
       have_ray = false;
@@ -936,12 +941,12 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     atomicAdd(A.stats + 5, st_disc);
     atomicAdd(A.stats + 6, st_wave_iters);
     atomicAdd(A.stats + 7, st_cull_lanes);
-    atomicAdd(A.stats + 16, st_cull_iters);
+    atomicAdd(A.stats + 8, st_cull_iters);
   }
   if constexpr (MODE == 2) {
     RTW_STAMP(4)
     if (lid == 0)
-      for (int i = 0; i < 6; ++i) atomicAdd(A.stats + 8 + i, (unsigned long long)ph[i]);
+      for (int i = 0; i < 10; ++i) atomicAdd(A.stats + 16 + i, (unsigned long long)ph[i]);
   }
 }
 
@@ -991,6 +996,7 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 20: launch_var<R, F32, 20>(a, grid, lds, s, mode); break;
     case 68: launch_var<R, F32, 68>(a, grid, lds, s, mode); break;
     case 72: launch_var<R, F32, 72>(a, grid, lds, s, mode); break;
+    case 40: launch_var<R, F32, 40>(a, grid, lds, s, mode); break;
 #endif
     case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
     case 8: launch_var<R, F32, 8>(a, grid, lds, s, mode); break;
@@ -1026,7 +1032,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #define RTW_OCC_CASE(v) \
   case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
 #ifndef RTW_ISA_QUICK
-    RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72)
+    RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
     RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8)
 #undef RTW_OCC_CASE

@@ -94,8 +94,8 @@ int main(int argc, char** argv) {
       const float aa = prec == 0 ? (float)a : af32;
       const rtwc::LaneCull lc = rtwc::lane_cull(of[0], of[1], of[2], aa, cmax);
       if (!lc.ok) continue;
-      const float x = rtwc::cull_x(of[0], of[1], of[2], df[0], df[1], df[2], aa, lc.alpha, fr, c0f[0], c0f[1],
-                                   c0f[2], -dcf[0], -dcf[1], -dcf[2], -(rf * rf), rho, moving);
+      const float x = rtwc::cull_x(of[0], of[1], of[2], df[0], df[1], df[2], rtwc::lane_const(aa, lc.alpha, rho), fr,
+                                   c0f[0], c0f[1], c0f[2], -dcf[0], -dcf[1], -dcf[2], -(rf * rf), moving);
       const bool exact_neg = prec == 0 ? (disc64 < 0) : (disc32 < 0);
       if (x < 0) {
         if (prec == 0) ++skipped;
