@@ -54,6 +54,20 @@ def parse():
     return ap.parse_args()
 
 
+def traffic_per_launch(args, W, H, spp):
+    """HBM bytes per trace launch from the committed PMC passes of the same
+    config (profiles/r01/traffic.json, tools/gpu_bench_profile.sh), else None."""
+    path = os.path.join(REPO, "profiles", "r01", "traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = t.get("config", {})
+    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision):
+        return None
+    return round(t["traffic_bytes_per_launch"])
+
+
 def cpu_baseline(width, height, spp_sample):
     """Oracle Tier A (the reference's render loop restated: f64, one sequential
     DefaultPrng(42) stream, recursive rayColor) on one core, on the same frame
@@ -163,7 +177,7 @@ def main():
         "bound": "valu-fp64" if args.precision == "f64" else "valu-fp32",
         "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
         "frac": round(achieved_tf / peak, 4),
-        "traffic": None,
+        "traffic": traffic_per_launch(args, W, H, spp),
         "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
         "flop_per_launch": flops, "segments_per_launch": counts["segments"],
         "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
