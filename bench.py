@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--engine", default="megakernel", choices=["megakernel", "wavefront"],
+                    help="headline engine (the other one is reported as a variant)")
+    ap.add_argument("--wf-paths", type=int, default=0, help="wavefront in-flight paths (0 = library default)")
+    ap.add_argument("--no-wavefront-variant", action="store_true")
     ap.add_argument("--spp", type=int, default=SPP, help="spp per GPU (default 500 = configs[1])")
     ap.add_argument("--width", type=int, default=W_IMG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,6 +93,61 @@ def cpu_baseline(width, height, spp_sample):
                       f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
 
 
+def wavefront_bytes(counts, precision, units):
+    """Algorithmic HBM bytes of one wavefront frame (rtw_wavefront.hip): per
+    bounce segment, extend reads o, d, time (+ the skip word in f32) and
+    writes (root, winner); shade reads the path + (root, winner) and writes
+    the path.  Per sample: the home slot's unit, sample index and f64x3 sum
+    (read + write).  Per unit: the f64x3 chunk sum."""
+    r = 8 if precision == "f64" else 4
+    path = 10 * r + 8 + 4 + 4
+    seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
+    return counts["segments"] * seg + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
+
+
+def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, samples_all, world, rank, dist,
+                      gather_image, torch):
+    """configs[3]: the same frame on the wavefront engine (bit-identical image,
+    tests/test_gpu_wavefront.py), timed the same way; roofline = HBM (the
+    path queues stream through HBM every bounce)."""
+    p = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
+                      precision=args.precision, engine="wavefront", wf_paths=args.wf_paths)
+    for _ in range(max(1, args.warmup)):
+        rend.render(cam, p, out=out)
+    torch.cuda.synchronize()
+    timers = [R.Timer() for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    a = time.perf_counter()
+    for i in range(args.steps):
+        rend.render(cam, p, out=out, timer=timers[i])
+        if world > 1:
+            gather_image(out, H, rank, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    e = time.perf_counter() - a
+    if world > 1:
+        t = torch.tensor([e], dtype=torch.float64, device=out.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e = float(t.item())
+    ms = sum(t.elapsed_ms() for t in timers) / len(timers)
+    for t in timers:
+        t.close()
+    chunk = min(R.DEFAULT_CHUNK, spp)
+    units = rc * W * ((spp + chunk - 1) // chunk)
+    byts = wavefront_bytes(counts, args.precision, units)
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
+            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                         "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
+                         "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts},
+            "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
+                    "same Tier-B image as the megakernel, bit for bit"}
+
+
 def main():
     args = parse()
     import torch
@@ -116,13 +175,14 @@ def main():
     cam = R.cover_camera(ASPECT)
     rb, rs, rc = shard_rows(H, rank, world)
     params = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
-                           precision=args.precision)
+                           precision=args.precision, engine=args.engine, wf_paths=args.wf_paths)
     rend = TorchRenderer(sph, mats, local)
     out = torch.empty((rc, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
     samples_rank = rc * W * spp
 
     # Untimed: counts pass (algorithmic flops of one trace launch) + warmup.
-    counts = rend.counts(cam, params)
+    counts = rend.counts(cam, R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
+                                            precision=args.precision))
     for _ in range(args.warmup):
         rend.render(cam, params, out=out)
         if world > 1:
@@ -211,6 +271,10 @@ def main():
                                        "ms_per_step": round(e32 / args.steps * 1e3, 3),
                                        "note": "precision=f32 (f32 + f64 wide spheres + convex self-skip); "
                                                "not the headline: the reference computes in f64"}
+
+    if not args.no_wavefront_variant and args.engine == "megakernel":
+        extra["wavefront_variant"] = wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts,
+                                                       samples_all, world, rank, dist, gather_image, torch)
 
     res = {
         "metric": "Msamples/sec (pixels x spp / s), RTIOW cover scene; trace-kernel roofline",

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 typedef enum {
   RTW_OK = 0,
@@ -78,6 +78,12 @@ typedef enum {
   RTW_PRECISION_F32 = 1       /* f32 + f64 for radius >= 100 spheres + convex self-skip */
 } rtw_precision;
 
+/* Render engine (both compute the same Tier-B image, bit for bit). */
+typedef enum {
+  RTW_ENGINE_MEGAKERNEL = 0,  /* one persistent trace kernel (BASELINE.json configs[1]) */
+  RTW_ENGINE_WAVEFRONT = 1    /* per-bounce kernels over SoA path queues in HBM (configs[3]) */
+} rtw_engine;
+
 typedef struct {
   uint32_t width, height;     /* full image (main.zig:305-306) */
   uint32_t spp;               /* samples_per_pixel (main.zig:308) */
@@ -90,9 +96,12 @@ typedef struct {
   uint32_t chunk;             /* samples per accumulation chunk, 0 = default (RTW_DEFAULT_CHUNK) */
   uint32_t precision;         /* rtw_precision */
   int32_t device;             /* HIP device for rtw_render (-1 = current) */
+  uint32_t engine;            /* rtw_engine */
+  uint32_t wf_paths;          /* wavefront: in-flight paths (queue capacity), 0 = RTW_DEFAULT_WF_PATHS */
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u
+#define RTW_DEFAULT_WF_PATHS (1u << 20)
 #define RTW_MAX_SPHERES 4096u
 
 /* ------------------------------------------------------------ queries -- */
@@ -143,7 +152,11 @@ int rtw_timer_elapsed_ms(rtw_timer t, float *ms); /* waits for the stop event */
  * DEVICE buffers d_rgb (W*row_count*3 bytes) and optional d_mean
  * (W*row_count*3 floats).  workspace: >= rtw_workspace_bytes(params) bytes
  * of device memory, 256-byte aligned.  timer (optional) brackets the trace
- * kernel.  Graph-capturable (no allocation, no synchronisation). */
+ * kernel.  Megakernel engine: graph-capturable (no allocation, no
+ * synchronisation).  Wavefront engine: the host polls the queue length
+ * between batches of bounce kernels, so the call returns after the last
+ * bounce kernel was ENQUEUED (the finalize kernel is still asynchronous) and
+ * it cannot be captured into a graph; the timer brackets all its kernels. */
 int rtw_render_device(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                       void *workspace, size_t workspace_bytes, uint8_t *d_rgb, float *d_mean,
                       void *stream, rtw_timer timer);

@@ -336,6 +336,11 @@ int validate(const rtw_params* p) {
     return fail(RTW_EINVAL, "rows %u + k*%u (k < %u) exceed height %u", p->row_begin, p->row_stride,
                 p->row_count, p->height);
   if (p->precision > RTW_PRECISION_F32) return fail(RTW_EINVAL, "precision %u", p->precision);
+  if (p->engine > RTW_ENGINE_WAVEFRONT) return fail(RTW_EINVAL, "engine %u", p->engine);
+  if (p->engine == RTW_ENGINE_WAVEFRONT && (p->wf_paths > (1u << 28) || (p->wf_paths && p->wf_paths < 64)))
+    return fail(RTW_EINVAL, "wf_paths %u outside [64, 2^28]", p->wf_paths);
+  if (p->engine == RTW_ENGINE_WAVEFRONT && p->max_depth > 0xFFFFu)
+    return fail(RTW_UNSUPPORTED, "wavefront engine: max_depth %u > 65535", p->max_depth);
   const uint64_t tiles = (uint64_t)((p->width + rtwk::kTileW - 1) / rtwk::kTileW) *
                          ((p->row_count + rtwk::kTileH - 1) / rtwk::kTileH);
   const uint64_t units = tiles * 64ull * n_chunks(p);
@@ -345,16 +350,34 @@ int validate(const rtw_params* p) {
   return RTW_OK;
 }
 
+uint32_t wf_paths(const rtw_params* p) { return p->wf_paths ? p->wf_paths : RTW_DEFAULT_WF_PATHS; }
+
+// Workspace: partial chunk sums | counters (unit queue head, wavefront queue
+// lengths) | stats | wavefront region (engine 1 only, rtw_internal.hpp
+// WfArgs): two path queues, the hit arrays, the home slots.
 struct WsLayout {
-  size_t partial_off, partial_bytes, counter_off, stats_off, total;
+  size_t partial_off, partial_bytes, counter_off, count_a_off, count_b_off, stats_off;
+  size_t wf_off, wf_queue_bytes, total;
 };
+size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+// Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk).
+size_t wf_queue_bytes(size_t n, size_t r) { return 10 * al256(n * r) + al256(n * 8) + 2 * al256(n * 4); }
 WsLayout ws_layout(const rtw_params* p) {
   WsLayout w;
   w.partial_off = 0;
   w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
-  w.counter_off = (w.partial_bytes + 255) & ~(size_t)255;
+  w.counter_off = al256(w.partial_bytes);
+  w.count_a_off = w.counter_off + 64;
+  w.count_b_off = w.counter_off + 128;
   w.stats_off = w.counter_off + 256;
   w.total = w.stats_off + 256;  // stats: 32 x u64
+  w.wf_off = w.total;
+  w.wf_queue_bytes = 0;
+  if (p->engine == RTW_ENGINE_WAVEFRONT) {
+    const size_t n = wf_paths(p), r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
+    w.wf_queue_bytes = wf_queue_bytes(n, r);
+    w.total += 2 * w.wf_queue_bytes + al256(n * r) + al256(n * 4) + al256(n * 24) + 2 * al256(n * 4);
+  }
   return w;
 }
 
@@ -406,6 +429,150 @@ size_t lds_bytes(const rtw_scene_s* sc, int prec) {
          4 * ((size_t)sc->n + 1 + sc->nm + sc->n) + 16;
 }
 
+// ---------------------------------------------------------- wavefront ----
+template <typename R>
+struct WfLaunch;
+template <>
+struct WfLaunch<double> {
+  static hipError_t gen(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_generate_f64(a, g, l, s);
+  }
+  static hipError_t ext(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_extend_f64(a, g, l, s);
+  }
+  static hipError_t shd(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_shade_f64(a, g, l, s);
+  }
+};
+template <>
+struct WfLaunch<float> {
+  static hipError_t gen(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_generate_f32(a, g, l, s);
+  }
+  static hipError_t ext(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_extend_f32(a, g, l, s);
+  }
+  static hipError_t shd(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_shade_f32(a, g, l, s);
+  }
+};
+
+template <typename R>
+rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
+  rtwk::PathBuf<R> q;
+  R** arr[10] = {&q.ox, &q.oy, &q.oz, &q.dx, &q.dy, &q.dz, &q.tx, &q.ty, &q.tz, &q.tm};
+  for (R** a : arr) {
+    *a = reinterpret_cast<R*>(b);
+    b += al256(n * sizeof(R));
+  }
+  q.rs = reinterpret_cast<uint64_t*>(b);
+  b += al256(n * 8);
+  q.slot = reinterpret_cast<uint32_t*>(b);
+  b += al256(n * 4);
+  q.dsk = reinterpret_cast<uint32_t*>(b);
+  b += al256(n * 4);
+  return q;
+}
+
+// Thread-local pinned words the host polls for the queue length.
+uint32_t* poll_words() {
+  thread_local uint32_t* w = nullptr;
+  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * sizeof(uint32_t), hipHostMallocPortable) != hipSuccess)
+    w = nullptr;
+  return w;
+}
+
+// Wavefront render: generate, then batches of kWfIters (extend, shade)
+// pairs; after each batch the live-path count of queue A is copied to pinned
+// memory, and the host stops once a batch (checked one batch behind, so the
+// GPU never idles on the poll) left the queue empty.  Empty batches cost
+// only the launches: every kernel reads its queue length first.
+constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
+template <typename R>
+int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned char* ws, const WsLayout& L, int dev,
+                  size_t lds, hipStream_t stream) {
+  if (ta.max_depth == 0) {  // rayColor(depth 0) is black (main.zig:105-108): no segment to trace
+    HIP_TRY(hipMemsetAsync(ws + L.partial_off, 0, L.partial_bytes, stream));
+    return RTW_OK;
+  }
+  const size_t n = wf_paths(p);
+  rtwk::WfArgs<R> a;
+  std::memset(&a, 0, sizeof(a));
+  a.t = ta;
+  unsigned char* b = ws + L.wf_off;
+  const rtwk::PathBuf<R> qa = carve_queue<R>(b, n), qb = carve_queue<R>(b, n);
+  a.hit_t = reinterpret_cast<R*>(b);
+  b += al256(n * sizeof(R));
+  a.hit_k = reinterpret_cast<int32_t*>(b);
+  b += al256(n * 4);
+  a.home_sum = reinterpret_cast<double*>(b);
+  b += al256(n * 24);
+  a.home_unit = reinterpret_cast<uint32_t*>(b);
+  b += al256(n * 4);
+  a.home_s = reinterpret_cast<uint32_t*>(b);
+  a.n_slots = (uint32_t)n;
+  uint32_t* cnt_a = reinterpret_cast<uint32_t*>(ws + L.count_a_off);
+  uint32_t* cnt_b = reinterpret_cast<uint32_t*>(ws + L.count_b_off);
+  const int prec = sizeof(R) == 4 ? 1 : 0;
+  const uint32_t cus = (uint32_t)device_cus(dev);
+  const uint32_t want = (uint32_t)((n + rtwk::kTraceBlock - 1) / rtwk::kTraceBlock);
+  auto grid_of = [&](int k, size_t l) {
+    static thread_local int bpc[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    static thread_local size_t bpc_lds[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    if (bpc[prec][k] == 0 || bpc_lds[prec][k] != l) {
+      bpc[prec][k] = rtwk::wf_blocks_per_cu(prec, k, l);
+      bpc_lds[prec][k] = l;
+    }
+    return std::max(1u, std::min(cus * (uint32_t)bpc[prec][k], want));
+  };
+  const uint32_t g_gen = grid_of(0, 0), g_ext = grid_of(1, lds), g_shd = grid_of(2, lds);
+  // generate -> queue A
+  a.out = qa;
+  a.count_out = cnt_a;
+  hipError_t e = WfLaunch<R>::gen(a, g_gen, 0, stream);
+  if (e != hipSuccess) return fail(RTW_EHIP, "wavefront generate launch: %s", hipGetErrorString(e));
+  uint32_t* poll = poll_words();
+  if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (auto& x : ev)
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return fail(RTW_EHIP, "hipEventCreate failed");
+  // Termination bound (never reached by a correct kernel): every iteration
+  // advances every live path by one segment.
+  const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / kWfIters + 4;
+  int st = RTW_OK;
+  for (uint64_t batch = 0;; ++batch) {
+    for (int k = 0; k < kWfIters && st == RTW_OK; ++k) {
+      const bool even = (k & 1) == 0;
+      a.in = even ? qa : qb;
+      a.out = even ? qb : qa;
+      a.count_in = even ? cnt_a : cnt_b;
+      a.count_out = even ? cnt_b : cnt_a;
+      if ((e = WfLaunch<R>::ext(a, g_ext, lds, stream)) != hipSuccess ||
+          (e = WfLaunch<R>::shd(a, g_shd, lds, stream)) != hipSuccess)
+        st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
+    }
+    if (st == RTW_OK && (hipMemcpyAsync(&poll[batch & 1], cnt_a, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                         hipEventRecord(ev[batch & 1], stream) != hipSuccess))
+      st = fail(RTW_EHIP, "wavefront poll enqueue failed");
+    if (st != RTW_OK) break;
+    if (batch > 0) {
+      if (hipEventSynchronize(ev[(batch - 1) & 1]) != hipSuccess) {
+        st = fail(RTW_EHIP, "wavefront batch failed on the device");
+        break;
+      }
+      if (poll[(batch - 1) & 1] == 0u) break;
+    }
+    if (batch > max_batches) {
+      st = fail(RTW_EHIP, "wavefront queue did not drain after %llu batches", (unsigned long long)batch);
+      break;
+    }
+  }
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  (void)prec;
+  return st;
+}
+
 int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace, size_t ws_bytes,
                uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode) {
   const WsLayout L = ws_layout(p);
@@ -426,7 +593,21 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   uint32_t total_units = 0;
   hipError_t e;
   if (timer) HIP_TRY(hipEventRecord(timer->start, stream));
-  if (p->precision == RTW_PRECISION_F32) {
+  if (p->engine == RTW_ENGINE_WAVEFRONT) {
+    if (mode != 0) return fail(RTW_UNSUPPORTED, "statistics passes run on the megakernel engine");
+    int st;
+    if (p->precision == RTW_PRECISION_F32) {
+      rtwk::TraceArgs<float> a;
+      fill_args(a, sc->v32, cam, p, ws, L);
+      st = run_wavefront<float>(a, p, ws, L, dev, lds, stream);
+    } else {
+      rtwk::TraceArgs<double> a;
+      fill_args(a, sc->v64, cam, p, ws, L);
+      st = run_wavefront<double>(a, p, ws, L, dev, lds, stream);
+    }
+    if (st != RTW_OK) return st;
+    e = hipSuccess;
+  } else if (p->precision == RTW_PRECISION_F32) {
     rtwk::TraceArgs<float> a;
     fill_args(a, sc->v32, cam, p, ws, L);
     total_units = a.total_units;

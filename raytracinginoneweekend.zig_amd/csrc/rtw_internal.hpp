@@ -92,4 +92,49 @@ constexpr int kTraceBlock = 256;
 // Per-wave LDS slots of coop_reject (rtw_trace.hip CoopSlots: 64 x u64 + 64 x u32).
 constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;
 
+// ------------------------------------------------------ wavefront engine --
+// rtw_wavefront.hip (BASELINE.json configs[3]): the same Tier-B render as the
+// megakernel, split into per-bounce kernels over SoA path queues in HBM.
+// A path = one in-flight sample: its ray, attenuation product, time, RNG
+// state, depth and the home slot that owns its (pixel, chunk) unit.  Two
+// queues ping-pong: extend(in) writes the closest hit per queue position,
+// shade(in -> out) scatters, finishes samples, refills units/samples and
+// appends the live paths to `out` compactly (one atomic per wave).
+template <typename R>
+struct PathBuf {
+  R *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz, *tm;
+  uint64_t* rs;
+  uint32_t* slot;  // home slot
+  uint32_t* dsk;   // depth | (skip + 1) << 16
+};
+// Moving bytes per path (one PathBuf entry).
+template <typename R>
+constexpr size_t kPathBytes = 10 * sizeof(R) + 8 + 4 + 4;
+// Home bytes per slot: f64x3 chunk sum, unit id, sample index.
+constexpr size_t kHomeBytes = 24 + 4 + 4;
+
+template <typename R>
+struct WfArgs {
+  TraceArgs<R> t;  // MUST stay at offset 0: kargs<R>() reads it
+  PathBuf<R> in, out;
+  R* hit_t;         // [queue position of `in`] root of the winner
+  int32_t* hit_k;   // [queue position of `in`] table position of the winner, -1 = miss
+  double* home_sum; // [slot][3]
+  uint32_t* home_unit;
+  uint32_t* home_s;
+  uint32_t* count_in;   // live paths in `in`
+  uint32_t* count_out;  // live paths appended to `out` (extend zeroes it)
+  uint32_t n_slots;
+  uint32_t pad;
+};
+
+hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_extend_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_extend_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
+// Resident workgroups per CU: kernel 0 = generate, 1 = extend, 2 = shade.
+int wf_blocks_per_cu(int precision, int kernel, size_t lds);
+
 }  // namespace rtwk

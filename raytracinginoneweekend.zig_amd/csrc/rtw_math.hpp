@@ -36,7 +36,7 @@ constexpr double kSinSignMax = 524288.0;                // 2^19
 // Out-of-range arguments (|a| >= 2^19, not produced by the cover scene): libm.
 // Kept out of line so its constants do not occupy registers of the kernel.
 #if defined(__HIPCC__)
-__host__ __device__ __noinline__
+static __host__ __device__ __noinline__
 #else
 inline
 #endif

@@ -26,436 +26,10 @@
 // The oracle's tierb_core.h is the written contract this file implements.
 #include <hip/hip_runtime.h>
 
-#include "rtw_cull.hpp"
-#include "rtw_internal.hpp"
-#include "rtw_math.hpp"
+#include "rtw_device.hpp"
 
 namespace rtwk {
 
-// ------------------------------------------------------------------ vec --
-template <typename R>
-struct V3 {
-  R x, y, z;
-};
-template <typename R>
-__device__ __forceinline__ V3<R> mk(R x, R y, R z) {
-  return V3<R>{x, y, z};
-}
-template <typename R>
-__device__ __forceinline__ V3<R> add(V3<R> a, V3<R> b) {
-  return mk(a.x + b.x, a.y + b.y, a.z + b.z);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> sub(V3<R> a, V3<R> b) {
-  return mk(a.x - b.x, a.y - b.y, a.z - b.z);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> mul(V3<R> a, R t) {
-  return mk(a.x * t, a.y * t, a.z * t);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> mulv(V3<R> a, V3<R> b) {
-  return mk(a.x * b.x, a.y * b.y, a.z * b.z);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> divs(V3<R> a, R t) {
-  return mk(a.x / t, a.y / t, a.z / t);
-}
-template <typename R>
-__device__ __forceinline__ R dot(V3<R> a, V3<R> b) {
-  return a.x * b.x + a.y * b.y + a.z * b.z;  // vec.zig:20-22, left to right
-}
-template <typename R>
-__device__ __forceinline__ R norm2(V3<R> a) {
-  return a.x * a.x + a.y * a.y + a.z * a.z;
-}
-template <typename R>
-__device__ __forceinline__ V3<R> normalized(V3<R> v) {  // vec.zig:32-39
-  const R n = sqrt(norm2(v));
-  return (n == (R)0) ? v : divs(v, n);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> ld3(const R* p) {
-  return mk(p[0], p[1], p[2]);
-}
-template <typename R>
-__device__ __forceinline__ V3<R> ld3(const __attribute__((address_space(4))) R* p) {
-  return mk(p[0], p[1], p[2]);
-}
-
-// ------------------------------------------------------------------ RNG --
-// Counter-based Zig std.Random.SplitMix64: sample (pixel p, sample s) owns the
-// 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its
-// draws are SplitMix64.next() from there, turned into reals by Zig's
-// Random.float (oracle/rtw_oracle.c tierb_state / ro_sm_f64 / ro_sm_f32).
-// Every draw is exactly one Weyl step: the rare extra words Random.float needs
-// for a tiny value come from the draw's own extension stream
-// SplitMix64.init(state ^ kExt), so draw k of a block sits at state
-// W + (k + 1) * gamma and any lane can evaluate any draw (coop_reject).
-constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
-constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
-__device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
-  st += kGamma;
-  return sm_mix(st);
-}
-__device__ __forceinline__ uint32_t clz64(uint64_t v) { return v ? (uint32_t)__clzll((long long)v) : 64u; }
-
-__device__ __forceinline__ uint32_t f64_long_lz(uint64_t draw_state) {  // probability 2^-12 per draw
-  uint64_t st = draw_state ^ kExt;
-  uint32_t lz = 12;
-  for (;;) {
-    const uint32_t addl = clz64(sm_next(st));
-    lz += addl;
-    if (addl != 64) break;
-    if (lz >= 1022) {
-      lz = 1022;
-      break;
-    }
-  }
-  return lz;
-}
-__device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
-  const uint64_t v = sm_next(st);
-  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-  // exponent = 1022 - clz(v); mantissa = low 52 bits.  Common case: the
-  // leading one is in the top 12 bits, i.e. in `hi`.
-  uint32_t lz = (uint32_t)__clz((int)hi);
-  if (__builtin_expect(hi < 0x00100000u, 0)) lz = f64_long_lz(st);
-  const uint32_t bhi = ((1022u - lz) << 20) | (hi & 0x000FFFFFu);
-  return __hiloint2double((int)bhi, (int)lo);
-}
-__device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
-  const uint64_t v = sm_next(st);
-  uint32_t lz = clz64(v);
-  if (__builtin_expect(lz >= 41, 0)) {  // probability 2^-41
-    uint64_t ext = st ^ kExt;
-    lz = 41 + clz64(sm_next(ext));
-    if (lz == 41 + 64) lz += (uint32_t)__clz((int)((uint32_t)sm_next(ext) | 0x7FFu));
-  }
-  const uint32_t bits = ((126u - lz) << 23) | ((uint32_t)v & ((1u << 23) - 1));
-  return __uint_as_float(bits);
-}
-template <typename R>
-__device__ __forceinline__ R rnd(uint64_t& st);
-template <>
-__device__ __forceinline__ double rnd<double>(uint64_t& st) {
-  return rnd_f64(st);
-}
-template <>
-__device__ __forceinline__ float rnd<float>(uint64_t& st) {
-  return rnd_f32(st);
-}
-template <typename R>
-__device__ __forceinline__ R rrange(uint64_t& st, R mn, R mx) {  // rand.zig:18-20
-  return mn + rnd<R>(st) * (mx - mn);
-}
-// randomReal(-1, 1) = -1 + r*2: r*2 is exact, so one FMA rounds identically.
-template <typename R>
-__device__ __forceinline__ R rrange_m11(uint64_t& st) {
-  return fma(rnd<R>(st), (R)2, (R)-1);
-}
-
-// ------------------------------------------------------------- kernel ----
-// Scene tables read with a wave-uniform index are accessed through the
-// constant address space (4): the compiler may then use scalar loads (s_load
-// into SGPRs) although the kernel also stores to global memory.
-#define RTW_CONST __attribute__((address_space(4)))
-template <typename T>
-__device__ __forceinline__ const RTW_CONST T* cptr(const T* p) {
-  return (const RTW_CONST T*)(p);
-}
-// A pointer the compiler cannot see through: loads through it are issued
-// where they are written (not hoisted into loop-invariant SGPRs), which keeps
-// the camera block out of the SGPR budget of the sphere loop.
-template <typename T>
-__device__ __forceinline__ const RTW_CONST T* opaque(const RTW_CONST T* p) {
-  asm volatile("" : "+s"(p));
-  return p;
-}
-// The kernel's only argument (TraceArgs) sits at offset 0 of the kernarg segment.
-template <typename R>
-__device__ __forceinline__ const RTW_CONST TraceArgs<R>* kargs() {
-  return (const RTW_CONST TraceArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr();
-}
-
-// ---------------------------------------------------- packed-f32 pretest --
-// Two spheres per v_pk_fma_f32 (rtw_cull.hpp: the bound and the scalar
-// statement of the same operations).  Record of pair p (64 B, scalar-loaded):
-// {c.x, c.y, c.z, ndc.x, ndc.y, ndc.z, nr2, unused}, each as {sphere 2p, 2p+1}.
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-struct PairRec {
-  f2 v[8];
-};
-__device__ __forceinline__ PairRec ld_pair(const __attribute__((address_space(4))) f2* t, uint32_t p) {
-  PairRec r;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = t[8 * p + i];
-  return r;
-}
-template <bool MOVING>
-__device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, f2 na, f2 k,
-                                        f2 frac) {
-  const f2* P = R_.v;
-  f2 ocx = ox - P[0], ocy = oy - P[1], ocz = oz - P[2];
-  if constexpr (MOVING) {
-    ocx = pfma(P[3], frac, ocx);
-    ocy = pfma(P[4], frac, ocy);
-    ocz = pfma(P[5], frac, ocz);
-  }
-  const f2 hb = pfma(ocz, dz, pfma(ocy, dy, ocx * dx));
-  const f2 cc = pfma(ocz, ocz, pfma(ocy, ocy, pfma(ocx, ocx, P[6])));
-  return pfma(na, cc, pfma(hb, hb, k));
-}
-
-template <typename R>
-struct Rec {  // one sphere record of the closest-hit loop
-  uint32_t meta;
-  R c[3], dc[3], r2;
-};
-
-template <typename R>
-struct Lane {
-  V3<R> o, d, T;
-  R time;
-  uint64_t rs;        // SplitMix64 Weyl state of the current sample
-  double sx, sy, sz;  // f64 chunk sum (main.zig:388-393 accumulates in f64)
-  uint32_t px, ly, c, s, s_end, depth;
-  int skip;
-};
-
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// ------------------------------------------------- cooperative rejection ----
-// The reference's rejection loops (rand.zig:22-28 randomPointInUnitSphere,
-// rand.zig:30-36 randomPointInUnitDisk) take the FIRST candidate inside the
-// unit ball.  Per lane that is ~1.9 (ball) / ~1.3 (disk) candidates, but a
-// wave waits for its unluckiest lane (~6.9 / ~3.6 wave iterations).  Because
-// candidate q of a D-dim loop whose state is B uses the draws at states
-// B + (D*q + i + 1) * gamma (one Weyl step per draw), the wave can instead
-// deal the candidates of its still-pending lanes to ALL 64 lanes: with m
-// pending lanes each gets c = 2^floor(log2(64/m)) candidates per round,
-// evaluated in parallel; the owner takes the lowest accepted one.  Same
-// candidate order, same result bits, ~3 rounds instead of ~7 iterations.
-// Must be called in wave-converged control flow (every lane of the wave).
-struct CoopSlots {
-  uint64_t st[64];  // pending lane's state B, by rank
-  uint32_t q[64];   // its next candidate index
-};
-constexpr size_t kCoopBytesPerWave = sizeof(CoopSlots);
-static_assert(kCoopBytesPerWave * (kTraceBlock / 64) == kCoopLdsBytes, "rtw_internal.hpp kCoopLdsBytes");
-
-template <typename R, int D>
-__device__ __forceinline__ bool in_unit_ball(const R (&x)[D]) {
-  if constexpr (D == 2)
-    return !(x[0] * x[0] + x[1] * x[1] + (R)0 * (R)0 >= (R)1);  // rand.zig:34: vec3(x, y, 0)
-  else
-    return !(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] >= (R)1);  // rand.zig:26; sqrt(t) >= 1 <=> t >= 1
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <typename R, int D, bool COOP>
-__device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], CoopSlots* slots, uint32_t lid) {
-  if constexpr (!COOP) {  // the literal per-lane loop (tuning variant 16)
-    if (need) {
-      for (;;) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) x[i] = rrange_m11<R>(st);
-        if (in_unit_ball<R, D>(x)) break;
-      }
-    }
-    return;
-  }
-  bool pending = false;
-  if (need) {  // round 0: every lane its own first candidate
-#pragma unroll
-    for (int i = 0; i < D; ++i) x[i] = rrange_m11<R>(st);
-    pending = !in_unit_ball<R, D>(x);
-  }
-  uint64_t P = __ballot(pending);
-  uint32_t nextq = 0;  // candidates are counted from B = st
-  while (P) {
-    const uint32_t m = (uint32_t)__popcll(P);
-    const uint32_t lc = 31u - (uint32_t)__clz((int)(64u / m));  // c = 2^lc, c*m <= 64
-    const uint32_t r = mbcnt64(P);
-    if (pending) {
-      slots->st[r] = st;
-      slots->q[r] = nextq;
-    }
-    wave_lds_sync();
-    const uint32_t orank = lid >> lc;
-    bool ok = false;
-    R y[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) y[i] = (R)0;
-    if (orank < m) {
-      uint64_t s = slots->st[orank] + (uint64_t)(D * (slots->q[orank] + (lid & ((1u << lc) - 1u)))) * kGamma;
-#pragma unroll
-      for (int i = 0; i < D; ++i) y[i] = rrange_m11<R>(s);
-      ok = in_unit_ball<R, D>(y);
-    }
-    const uint64_t acc = __ballot(ok);
-    wave_lds_sync();  // slots are rewritten next round
-    const uint32_t first = (r << lc) & 63u;  // pending lanes: r*c < 64
-    const uint64_t mine = lc == 6u ? acc : (acc >> first) & ((1ull << (1u << lc)) - 1ull);
-    const uint32_t jj = mine ? (uint32_t)__builtin_ctzll(mine) : 0u;
-    const int src = (int)(first + jj);
-    R z[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) z[i] = __shfl(y[i], src);
-    if (pending) {
-      if (mine) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) x[i] = z[i];
-        st += (uint64_t)(D * (nextq + jj + 1u)) * kGamma;
-        pending = false;
-      } else {
-        nextq += 1u << lc;
-      }
-    }
-    P = __ballot(pending);
-  }
-}
-
-// v / |v| with the three divisions done against RN(1/|v|) (rtw_math.hpp div_rn).
-template <typename R>
-__device__ __forceinline__ V3<R> normalized_rn(V3<R> v) {  // vec.zig:32-39
-  const R n = sqrt(norm2(v));
-  if (n == (R)0) return v;
-  const R y = (R)1 / n;
-  return mk(rtwm::div_rn(v.x, n, y), rtwm::div_rn(v.y, n, y), rtwm::div_rn(v.z, n, y));
-}
-
-// Camera.getRay (main.zig:91-100) after the u,v jitter (main.zig:390-391).
-// Part 1: the sample's RNG block and the u, v jitter (main.zig:390-391).
-template <typename R>
-__device__ __forceinline__ void start_sample_uv(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, R& u, R& v) {
-  const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
-  const uint32_t y = A.row_begin + L.ly * A.row_stride;  // image row (top-first)
-  const uint32_t j = A.H - 1 - y;                        // reference row index
-  const uint64_t pixel = (uint64_t)y * A.W + L.px;
-  L.rs = A.seed_base + ((((pixel << 24) | (uint64_t)L.s)) << 16) * kGamma;
-  u = rtwm::div_rn((R)L.px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
-  v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
-}
-// Part 2, after the lens-disk point (rand.zig:30-36, coop_reject<R, 2>).
-template <typename R>
-__device__ __forceinline__ void start_sample_ray(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, R u, R v, R dx,
-                                                 R dy) {
-  const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
-  const V3<R> rd = mk(dx * A.lens_radius, dy * A.lens_radius, (R)0 * A.lens_radius);
-  const V3<R> cu = ld3(A.cu), cv = ld3(A.cv), org = ld3(A.origin);
-  const V3<R> offset = add(mul(cu, rd.x), mul(cv, rd.y));
-  L.d = sub(sub(add(add(ld3(A.llc), mul(ld3(A.horizontal), u)), mul(ld3(A.vertical), v)), org), offset);
-  L.o = add(org, offset);
-  L.time = rrange<R>(L.rs, A.time0, A.time1);
-  L.T = mk((R)1, (R)1, (R)1);
-  L.depth = 0;
-  L.skip = -1;
-}
-
-// f64 quadratic for a wide sphere in f32 mode (tierb_core.h TBF(test), wide
-// branch): the roots are solved in f64 and rounded to f32 before any
-// comparison, so a wide sphere competes with the others on f32 roots.
-// Returns false when the line misses (disc < 0); else `root` is the sphere's
-// effective root (root1 if root1 >= tmin, else root2).
-__device__ __forceinline__ bool wide_root(const RTW_CONST double* w, uint32_t meta, const RTW_CONST double* tgd,
-                                          V3<float> o, V3<float> d, float time, float tmin, float& root) {
-  double cx = w[0], cy = w[1], cz = w[2];
-  if (meta & kMoving) {
-    const uint32_t g = (meta >> 2) & 63u;
-    const double fr = ((double)time - tgd[4 * g]) / (tgd[4 * g + 1] - tgd[4 * g]);
-    cx = cx + w[3] * fr;
-    cy = cy + w[4] * fr;
-    cz = cz + w[5] * fr;
-  }
-  const double ox = (double)o.x - cx, oy = (double)o.y - cy, oz = (double)o.z - cz;
-  const double dx = d.x, dy = d.y, dz = d.z;
-  const double ad = dx * dx + dy * dy + dz * dz;
-  const double hb = ox * dx + oy * dy + oz * dz;
-  const double c = (ox * ox + oy * oy + oz * oz) - w[6];
-  const double disc = hb * hb - ad * c;
-  if (disc < 0.0) return false;
-  const double sq = sqrt(disc);
-  root = (float)((-hb - sq) / ad);
-  if (root < tmin) root = (float)((-hb + sq) / ad);
-  return true;
-}
-
-// The reference's literal closest-hit loop (hittable.zig:231-244 with
-// Sphere/MovingSphere.hit's root selection), in list order, from LDS tables;
-// used only for lanes that met a NaN in the grouped loops.
-template <typename R, bool F32>
-__device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* l_sph, const R* l_rad,
-                                             const uint32_t* l_meta, const R* l_tg, const uint32_t* l_perm,
-                                             const Lane<R>& L, R a, R tmin, R& tmax, int& hit) {
-  tmax = (R)__builtin_huge_val();
-  hit = -1;
-  for (uint32_t i = 0; i < S.n; ++i) {
-    const uint32_t k = l_perm[i];
-    const uint32_t meta = l_meta[k];
-    if (F32 && (int)k == L.skip) continue;
-    if constexpr (F32) {
-      if (meta & kWide) {
-        float root = 0.0f;
-        if (!wide_root(cptr(S.wide_d) + 8 * k, meta, cptr(S.tg_d), L.o, L.d, L.time, tmin, root)) continue;
-        if (root < tmin || tmax < root) continue;
-        tmax = root;
-        hit = (int)k;
-        continue;
-      }
-    }
-    const R* sp = l_sph + 8 * k;
-    R cx = sp[0], cy = sp[1], cz = sp[2];
-    if (meta & kMoving) {
-      const uint32_t g = (meta >> 2) & 63u;
-      const R fr = (L.time - l_tg[4 * g]) / (l_tg[4 * g + 1] - l_tg[4 * g]);
-      cx = cx + sp[3] * fr;
-      cy = cy + sp[4] * fr;
-      cz = cz + sp[5] * fr;
-    }
-    const R ocx = L.o.x - cx, ocy = L.o.y - cy, ocz = L.o.z - cz;
-    const R hb = ocx * L.d.x + ocy * L.d.y + ocz * L.d.z;
-    const R cc = (ocx * ocx + ocy * ocy + ocz * ocz) - sp[6];
-    const R disc = hb * hb - a * cc;
-    if (disc < (R)0) continue;
-    const R sq = sqrt(disc);
-    R root = (-hb - sq) / a;
-    if (root < tmin || tmax < root) {
-      root = (-hb + sq) / a;
-      if (root < tmin || tmax < root) continue;
-    }
-    tmax = root;
-    hit = (int)k;
-  }
-  (void)l_rad;
-}
-
-// Diagnostic phase stamps (MODE 2 only): s_memtime between phases, summed per
-// wave in SGPRs.  Never part of the product build's timing (rtw_render_counts).
-#define RTW_STAMP(slot)                                                          \
-  if constexpr (MODE == 2) {                                                     \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    uint64_t t_;                                                                 \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    ph[slot] += t_ - t_last;                                                     \
-    t_last = t_;                                                                 \
-  }
 
 // VAR (tuning variants, selected at launch): bit0 = sphere records from LDS
 // instead of scalar loads; bit1 = unroll the sphere loop by 2; bit2 = ask for
@@ -466,29 +40,14 @@ __device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* 
 template <typename R, bool F32, int MODE, int VAR>
 __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 1)) trace_kernel(TraceArgs<R> A) {
   constexpr bool STATS = MODE == 1;
-  constexpr bool CULL = !(VAR & 64);                // packed-f32 pretest for narrow spheres
   constexpr bool COOP = !(VAR & 16);               // unit-ball point (scatter)
   constexpr bool COOP_DISK = COOP && (VAR & 32);  // lens-disk point (camera ray)
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const SceneView<R> S = A.sc;
   // LDS: per-wave coop_reject slots, then copies of the per-lane lookup
   // tables (winning sphere, its material).
-  CoopSlots* slots = reinterpret_cast<CoopSlots*>(lds_raw) + (threadIdx.x >> 6);
-  R* l_sph = reinterpret_cast<R*>(lds_raw + kCoopBytesPerWave * (kTraceBlock / 64));
-  R* l_rad = l_sph + 8 * (S.n + 1);
-  R* l_mat = l_rad + S.n;
-  R* l_tg = l_mat + 8 * S.nm;
-  uint32_t* l_meta = reinterpret_cast<uint32_t*>(l_tg + 4 * S.ng);
-  uint32_t* l_kind = l_meta + S.n + 1;
-  uint32_t* l_perm = l_kind + S.nm;  // original list index -> table position
-  for (uint32_t i = threadIdx.x; i < 8 * (S.n + 1); i += blockDim.x) l_sph[i] = S.sph[i];
-  for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) l_rad[i] = S.rad[i];
-  for (uint32_t i = threadIdx.x; i < 8 * S.nm; i += blockDim.x) l_mat[i] = S.mat[i];
-  for (uint32_t i = threadIdx.x; i < 4 * S.ng; i += blockDim.x) l_tg[i] = S.tg[i];
-  for (uint32_t i = threadIdx.x; i < S.n + 1; i += blockDim.x) l_meta[i] = S.meta[i];
-  for (uint32_t i = threadIdx.x; i < S.nm; i += blockDim.x) l_kind[i] = S.kind[i];
-  for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) l_perm[i] = S.perm[i];
-  __syncthreads();
+  const LdsTables<R> T = stage_tables<R>(S, lds_raw);
+  CoopSlots* slots = T.slots;
 
   const uint32_t lid = lane_id();
   const uint32_t npix = A.row_count * A.W;
@@ -505,12 +64,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   bool have_ray = false;   // lane has a live path
   bool done = false;       // queue exhausted for this lane
   uint32_t qnext = 0, qend = 0;  // wave-uniform batch [qnext, qend)
-  unsigned long long st_samples = 0, st_segments = 0, st_skipped = 0;
-  unsigned long long st_candwave = 0, st_candlane = 0, st_disc = 0, st_wave_iters = 0;
-  unsigned long long st_cull_lanes = 0, st_cull_iters = 0;
-  uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t t_last = 0;
-  if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last)::"memory");
+  KStats st;
+  if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
 
   for (;;) {
     RTW_STAMP(5)
@@ -599,232 +154,11 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if (L.depth == A.max_depth) {  // rayColor depth == 0 (main.zig:105-108)
         ended = true;
       } else {
-        if (STATS) st_segments++;
+        if (STATS) st.segments++;
         if constexpr (STATS) {
-          if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_wave_iters++;
+          if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.wave_iters++;
         }
-        const R a = norm2(L.d);
-        const R inv_a = (R)1 / a;          // RN(1/a): roots via div_rn
-        const R pre_lim = A.pre_k * a;     // "both roots behind" prefilter bound
-        int tg_cur = -1;
-        R frac = (R)0;
-        const RTW_CONST uint32_t* c_meta = cptr(S.meta);
-        const RTW_CONST R* c_sph = cptr(S.sph);
-        const RTW_CONST R* c_tg = cptr(S.tg);
-        // HittableList.hit (hittable.zig:231-244): every lane tests sphere k
-        // together; the record comes through scalar loads.
-        // Closest hit.  The reference's sequential HittableList.hit returns the
-        // sphere of minimal effective root (root1 if root1 >= tmin, else root2;
-        // root2 >= root1 always), ties to the LAST in list order — an
-        // order-independent rule.  So the table is
-        // grouped [static-wide | static | moving-wide | moving] and each group
-        // runs as its own branch-free loop; ties compare original indices.
-        int hit_orig = -1;
-        bool nan_seen = false;
-        auto accept = [&](R root, int pos, int orig) {
-          if (root != root) nan_seen = true;  // NaN: sequential fallback below
-          if (!(root < tmin) & ((root < tmax) | ((root == tmax) & (orig > hit_orig)))) {
-            tmax = root;
-            hit = pos;
-            hit_orig = orig;
-          }
-        };
-        auto test = [&](uint32_t k, uint32_t meta, R cx, R cy, R cz, R r2) {
-          const R ocx = L.o.x - cx, ocy = L.o.y - cy, ocz = L.o.z - cz;
-          const R hb = ocx * L.d.x + ocy * L.d.y + ocz * L.d.z;
-          const R cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
-          const R disc = hb * hb - a * cc;
-          // Candidate unless disc < 0, or provably both roots < tmin: origin
-          // outside (cc > 0) and sphere behind (hb > 0) give root1 <= 0 and
-          // root2 <= ~2u*hb/a < tmin while hb < pre_k*a.
-          // One compare on the hot path; ~97 % of tests end here.  A NaN disc
-          // also enters (reference: `disc < 0` is false for NaN).
-          if (!(disc < (R)0)) {
-            // (bitwise &: no short-circuit branches)
-            const bool pre = (hb > (R)0) & (cc > (R)0) & (hb < pre_lim);
-            bool cand = !pre;
-            if (F32) cand = cand & ((int)k != L.skip);
-            if constexpr (STATS) {
-              const uint64_t cm = __ballot(cand);
-              if (cm && lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_candwave++;
-              st_candlane += cand ? 1 : 0;
-              st_disc += 1;
-            }
-            if (cand) {
-              const R sq = sqrt(disc);
-              R root = rtwm::div_rn(-hb - sq, a, inv_a);
-              if (root < tmin) root = rtwm::div_rn(-hb + sq, a, inv_a);
-              accept(root, (int)k, (int)(meta >> 20));
-            }
-          }
-        };
-        auto rec_at = [&](uint32_t k) {
-          Rec<R> r;
-          if constexpr (VAR & 1) {
-            const R* sp = l_sph + 8 * k;
-            r.meta = l_meta[k];
-            r.c[0] = sp[0], r.c[1] = sp[1], r.c[2] = sp[2], r.dc[0] = sp[3], r.dc[1] = sp[4], r.dc[2] = sp[5];
-            r.r2 = sp[6];
-          } else {
-            const RTW_CONST R* sp = c_sph + 8 * k;
-            r.meta = c_meta[k];
-            r.c[0] = sp[0], r.c[1] = sp[1], r.c[2] = sp[2], r.dc[0] = sp[3], r.dc[1] = sp[4], r.dc[2] = sp[5];
-            r.r2 = sp[6];
-          }
-          return r;
-        };
-        // f32 mode: wide spheres (radius >= 100), solved in f64.
-        if constexpr (F32) {
-          auto wide_range = [&](uint32_t b, uint32_t e) {
-            for (uint32_t k = b; k < e; ++k) {
-              const uint32_t meta = c_meta[k];
-              float root = 0.0f;
-              if ((int)k != L.skip && wide_root(cptr(S.wide_d) + 8 * k, meta, cptr(S.tg_d), L.o, L.d, L.time, tmin, root))
-                accept(root, (int)k, (int)(meta >> 20));
-            }
-          };
-          wide_range(0, S.g_static_wide);
-          wide_range(S.g_static, S.g_moving_wide);
-        }
-        // static spheres: records stream one step ahead (padding record at the end)
-        auto static_range = [&](uint32_t b, uint32_t e) {
-          if (b < e) {
-            Rec<R> cur = rec_at(b);
-#pragma unroll(((VAR & 2) ? 2 : 1))
-            for (uint32_t k = b; k < e; ++k) {
-              const Rec<R> nxt = rec_at(k + 1);
-              test(k, cur.meta, cur.c[0], cur.c[1], cur.c[2], cur.r2);
-              cur = nxt;
-            }
-          }
-        };
-        // moving spheres: centre(t) = c0 + (c1 - c0) * frac (hittable.zig:219-221)
-        auto moving_range = [&](uint32_t b, uint32_t e) {
-          if (b < e) {
-            Rec<R> cur = rec_at(b);
-#pragma unroll(((VAR & 2) ? 2 : 1))
-            for (uint32_t k = b; k < e; ++k) {
-              const Rec<R> nxt = rec_at(k + 1);
-              const int g = (int)((cur.meta >> 2) & 63u);
-              if (g != tg_cur) {  // wave-uniform: recomputed only when the time group changes
-                tg_cur = g;
-                frac = rtwm::div_rn(L.time - c_tg[4 * g], c_tg[4 * g + 1] - c_tg[4 * g], c_tg[4 * g + 2]);
-              }
-              test(k, cur.meta, cur.c[0] + cur.dc[0] * frac, cur.c[1] + cur.dc[1] * frac, cur.c[2] + cur.dc[2] * frac,
-                   cur.r2);
-              cur = nxt;
-            }
-          }
-        };
-        if (!CULL || !S.cull_on) {
-          static_range(F32 ? S.g_static_wide : 0u, S.g_static);
-          moving_range(F32 ? S.g_moving_wide : S.g_static, S.n);
-        } else {
-          if constexpr (!F32) {  // wide spheres: exact, wave-uniform
-            static_range(0u, S.g_static_wide);
-            moving_range(S.g_static, S.g_moving_wide);
-          }
-          // Narrow spheres: the packed-f32 pretest (rtw_cull.hpp) proves
-          // disc < 0 for most (lane, sphere) pairs; each lane then runs the
-          // exact test only on the spheres it could not rule out.
-          const float af = (float)a;
-          const rtwc::LaneCull lc = rtwc::lane_cull((float)L.o.x, (float)L.o.y, (float)L.o.z, af, S.cull_cmax);
-          const f2 ox = bc((float)L.o.x), oy = bc((float)L.o.y), oz = bc((float)L.o.z);
-          const f2 dx = bc((float)L.d.x), dy = bc((float)L.d.y), dz = bc((float)L.d.z);
-          const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, S.cull_rho);
-          const f2 na = bc(lk.na), alpha = bc(lk.k);
-          const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(S.cull));
-          const RTW_CONST uint32_t* ctg = cptr(S.cull_tg);
-          const RTW_CONST float* ctf = cptr(S.tg_f);
-          const float tf = (float)L.time;
-          const uint32_t np_static = S.n_sn >> 1;  // pairs with two static spheres
-          int fr_g = -1;  // phase B: time group of fr_v
-          R fr_v = (R)0;
-          for (uint32_t base = 0; base < S.nn; base += 64) {
-            uint32_t sk[2] = {0u, 0u};  // bit 31-r of sk[h]: sphere base+32h+r proven to miss
-            uint32_t tgp_cur = ~0u;
-            f2 fr2 = bc(0.0f);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const uint32_t p0 = (base >> 1) + 16u * h, p1 = min(p0 + 16u, (S.nn + 1u) >> 1);
-              // pair records stream one step ahead (the table has a padding pair)
-              if (p0 < p1) {
-                PairRec cur = ld_pair(ct, p0);
-                uint32_t tgp_nxt = ctg[p0];
-                for (uint32_t p = p0; p < p1; ++p) {
-                  const PairRec nxt = ld_pair(ct, p + 1);
-                  const uint32_t tgp = tgp_nxt;
-                  tgp_nxt = ctg[p + 1];
-                  f2 x;
-                  if (p < np_static) {
-                    x = cull_pair<false>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
-                  } else {
-                    if (tgp != tgp_cur) {  // wave-uniform
-                      tgp_cur = tgp;
-                      const uint32_t g0 = tgp & 0xFFu, g1 = tgp >> 8;
-                      fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
-                    }
-                    x = cull_pair<true>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
-                  }
-                  sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.x), 31);
-                  sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.y), 31);
-                  cur = nxt;
-                }
-              }
-              // fewer than 16 pairs: move sphere r of the chunk to bit 31 - r
-              const uint32_t cnt = p1 > p0 ? 2u * (p1 - p0) : 0u;
-              sk[h] = cnt == 0u ? 0u : (cnt == 32u ? sk[h] : sk[h] << (32u - cnt));
-            }
-            const uint32_t rem = S.nn - base;  // real spheres in this block
-            const uint32_t v0 = rem >= 32u ? ~0u : ~(~0u >> rem);
-            const uint32_t v1 = rem >= 64u ? ~0u : (rem <= 32u ? 0u : ~(~0u >> (rem - 32u)));
-            uint32_t m0 = v0, m1 = v1;
-            if (lc.ok) {
-              m0 &= ~sk[0];
-              m1 &= ~sk[1];
-            }
-            if constexpr (STATS) st_cull_lanes += __popc(m0) + __popc(m1);
-            RTW_STAMP(2)
-            while (m0 | m1) {  // per lane: the exact test on the survivors
-              if constexpr (STATS) {
-                if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st_cull_iters++;
-              }
-              uint32_t r;
-              if (m0) {
-                r = __clz(m0);
-                m0 &= ~(0x80000000u >> r);
-              } else {
-                r = __clz(m1);
-                m1 &= ~(0x80000000u >> r);
-                r += 32u;
-              }
-              const uint32_t j = base + r;
-              const uint32_t k = j < S.n_sn ? S.g_static_wide + j : S.g_moving_wide + (j - S.n_sn);
-              const R* sp = l_sph + 8 * k;
-              const uint32_t meta = l_meta[k];
-              R cx = sp[0], cy = sp[1], cz = sp[2];
-              if (meta & kMoving) {
-                const int g = (int)((meta >> 2) & 63u);
-                if (g != fr_g) {  // per lane: usually once per segment
-                  fr_g = g;
-                  fr_v = rtwm::div_rn(L.time - l_tg[4 * g], l_tg[4 * g + 1] - l_tg[4 * g], l_tg[4 * g + 2]);
-                }
-                cx = cx + sp[3] * fr_v;
-                cy = cy + sp[4] * fr_v;
-                cz = cz + sp[5] * fr_v;
-              }
-              test(k, meta, cx, cy, cz, sp[6]);
-            }
-            RTW_STAMP(6)
-          }
-        }
-        // A NaN anywhere makes the reference's acceptance order-dependent:
-        // redo such lanes with its literal sequential loop.
-        if (__builtin_expect(__any(nan_seen), 0)) {
-          if (nan_seen) seq_closest_hit<R, F32>(S, l_sph, l_rad, l_meta, l_tg, l_perm, L, a, tmin, tmax, hit);
-        }
-        if (STATS && L.skip >= 0) st_skipped++;
-        RTW_STAMP(2)
+        closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
 
         if (hit < 0) {  // miss: background (main.zig:109-112)
           const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
@@ -833,7 +167,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           L.sz += (double)col.z;
           ended = true;
         } else {
-          kind = l_kind[(l_meta[hit] >> 8) & 0xFFFu];
+          kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
           shading = true;
         }
       }
@@ -846,83 +180,14 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if (__any(nb)) coop_reject<R, 3, COOP>(nb, L.rs, b3, slots, lid);
       RTW_STAMP(7)
       if (shading) {
-          // Hit record of the winner (hittable.zig:118-128, :189-198).
-          const R* sp = l_sph + 8 * hit;
-          const uint32_t meta = l_meta[hit];
-          const V3<R> p = add(L.o, mul(L.d, tmax));
-          V3<R> center = ld3(sp);
-          if (meta & kMoving) {
-            const uint32_t g = (meta >> 2) & 63u;
-            const R fr = rtwm::div_rn(L.time - l_tg[4 * g], l_tg[4 * g + 1] - l_tg[4 * g], l_tg[4 * g + 2]);
-            center = add(center, mul(ld3(sp + 3), fr));
-          }
-          const R rad = l_rad[hit], inv_r = sp[7];
-          const V3<R> q = sub(p, center);
-          const V3<R> outward = mk(rtwm::div_rn(q.x, rad, inv_r), rtwm::div_rn(q.y, rad, inv_r),
-                                   rtwm::div_rn(q.z, rad, inv_r));
-          const bool front = dot(outward, L.d) < (R)0;
-          const V3<R> normal = front ? outward : mul(outward, (R)-1);
-          const R* mp = l_mat + 8 * ((meta >> 8) & 0xFFFu);
-          // Material.scatter (material.zig:22-29), lanes of one kind together.
-          // One normalisation per lane: the unit-ball point (Lambertian) or the
-          // ray direction (Metal, Dielectric).
-          const V3<R> rs = mk(b3[0], b3[1], b3[2]);
-          const V3<R> nv = normalized_rn(kind <= 1u ? rs : L.d);
-          const V3<R> ud = nv;
-          V3<R> ndir, att;
-          bool absorbed = false;
-          if (kind <= 1u) {  // Lambertian (material.zig:44-52)
-            ndir = add(normal, nv);
-            if (fabs(ndir.x) < (R)1e-8 && fabs(ndir.y) < (R)1e-8 && fabs(ndir.z) < (R)1e-8) ndir = normal;
-            att = ld3(mp);
-            // CheckerTexture.value (texture.zig:79-82): only the sign matters.
-            if (kind == 1u && rtwm::checker_odd((double)((R)10 * p.x), (double)((R)10 * p.y), (double)((R)10 * p.z)))
-              att = ld3(mp + 3);
-          } else if (kind == 2u) {  // Metal (material.zig:59-65)
-            const V3<R> refl = sub(ud, mul(normal, (R)2 * dot(ud, normal)));
-            ndir = add(refl, mul(rs, mp[6]));
-            att = ld3(mp);
-            absorbed = !(dot(refl, normal) > (R)0);
-          } else {  // Dielectric (material.zig:72-91); mp[6] = RN(1/ir)
-            const R ir = mp[7];
-            const R ratio = front ? mp[6] : ir;
-            const R cos_t = fmin(dot(mul(ud, (R)-1), normal), (R)1);
-            const R sin_t = sqrt((R)1 - cos_t * cos_t);
-            bool refr = false;
-            if (ratio * sin_t <= (R)1) {
-              const R r0 = ((R)1 - ratio) / ((R)1 + ratio);
-              const R r1 = r0 * r0;
-              const R x = (R)1 - cos_t;
-              const R x2 = x * x;
-              const R refl_p = r1 + ((R)1 - r1) * (x * (x2 * x2));  // Zig pow(x, 5.0)
-              refr = refl_p < rnd<R>(L.rs);
-            }
-            if (refr) {  // refract (material.zig:116-121)
-              const R ct = fmin(dot(mul(ud, (R)-1), normal), (R)1);
-              const V3<R> perp = mul(add(ud, mul(normal, ct)), ratio);
-              const V3<R> par = mul(normal, -sqrt(fabs((R)1 - norm2(perp))));
-              ndir = add(perp, par);
-            } else {
-              ndir = sub(ud, mul(normal, (R)2 * dot(ud, normal)));
-            }
-            att = mk((R)1, (R)1, (R)1);
-          }
-          if (absorbed) {
-            ended = true;  // emitted == 0 (material.zig:31-38)
-          } else {
-            L.T = mulv(L.T, att);
-            if (F32) L.skip = (dot(ndir, outward) > (R)0) ? hit : -1;
-            L.o = p;
-            L.d = ndir;
-            L.depth++;
-          }
+        if (scatter_hit<R, F32>(T, L, hit, tmax, kind, b3)) ended = true;
       }
     }
     RTW_STAMP(8)
     if (ended) {  // (a miss added its colour above; depth limit and absorption add 0)
       L.s++;
       have_ray = false;
-      if (STATS) st_samples++;
+      if (STATS) st.samples++;
       if (L.s == L.s_end) {  // unit done: publish the chunk sum
         double* dst = A.partial + ((size_t)L.c * npix + (size_t)L.ly * A.W + L.px) * 3;
         dst[0] = L.sx;
@@ -933,20 +198,20 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     }
   }
   if (STATS) {
-    atomicAdd(A.stats + 0, st_samples);
-    atomicAdd(A.stats + 1, st_segments);
-    atomicAdd(A.stats + 2, st_skipped);
-    atomicAdd(A.stats + 3, st_candwave);
-    atomicAdd(A.stats + 4, st_candlane);
-    atomicAdd(A.stats + 5, st_disc);
-    atomicAdd(A.stats + 6, st_wave_iters);
-    atomicAdd(A.stats + 7, st_cull_lanes);
-    atomicAdd(A.stats + 8, st_cull_iters);
+    atomicAdd(A.stats + 0, st.samples);
+    atomicAdd(A.stats + 1, st.segments);
+    atomicAdd(A.stats + 2, st.skipped);
+    atomicAdd(A.stats + 3, st.candwave);
+    atomicAdd(A.stats + 4, st.candlane);
+    atomicAdd(A.stats + 5, st.disc);
+    atomicAdd(A.stats + 6, st.wave_iters);
+    atomicAdd(A.stats + 7, st.cull_lanes);
+    atomicAdd(A.stats + 8, st.cull_iters);
   }
   if constexpr (MODE == 2) {
     RTW_STAMP(4)
     if (lid == 0)
-      for (int i = 0; i < 10; ++i) atomicAdd(A.stats + 16 + i, (unsigned long long)ph[i]);
+      for (int i = 0; i < 10; ++i) atomicAdd(A.stats + 16 + i, (unsigned long long)st.ph[i]);
   }
 }
 

@@ -27,6 +27,8 @@ HEADER_PATH = os.path.join(REPO, "include", "rtw_hip.h")
 RTW_OK, RTW_EINVAL, RTW_UNSUPPORTED, RTW_EHIP, RTW_ENOMEM, RTW_ENODEV = 0, -1, -2, -3, -4, -5
 LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 PRECISION = {"f64": 0, "f32": 1}
+ENGINE = {"megakernel": 0, "wavefront": 1}
+DEFAULT_WF_PATHS = 1 << 20
 DEFAULT_CHUNK = 32
 COVER_BACKGROUND = (0.70, 0.80, 1.00)
 
@@ -57,7 +59,8 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32),
                 ("max_depth", C.c_uint32), ("seed", C.c_uint64), ("background", C.c_double * 3),
                 ("row_begin", C.c_uint32), ("row_stride", C.c_uint32), ("row_count", C.c_uint32),
-                ("chunk", C.c_uint32), ("precision", C.c_uint32), ("device", C.c_int32)]
+                ("chunk", C.c_uint32), ("precision", C.c_uint32), ("device", C.c_int32),
+                ("engine", C.c_uint32), ("wf_paths", C.c_uint32)]
 
 
 _lib = None
@@ -156,12 +159,14 @@ def cover_scene(seed: int = 42):
 
 
 def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACKGROUND, row_begin=0,
-                row_stride=1, row_count=None, chunk=0, precision="f64", device=-1) -> Params:
+                row_stride=1, row_count=None, chunk=0, precision="f64", device=-1, engine="megakernel",
+                wf_paths=0) -> Params:
     if row_count is None:
         row_count = (height - row_begin + row_stride - 1) // row_stride
     prec = PRECISION[precision] if isinstance(precision, str) else int(precision)
+    eng = ENGINE[engine] if isinstance(engine, str) else int(engine)
     return Params(width, height, spp, max_depth, seed, (C.c_double * 3)(*background), row_begin, row_stride,
-                  row_count, chunk, prec, device)
+                  row_count, chunk, prec, device, eng, wf_paths)
 
 
 def _arr(x, typ):

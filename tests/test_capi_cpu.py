@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol(rtw):
 
 
 def test_abi_version(rtw):
-    assert rtw.abi_version() == 1
+    assert rtw.abi_version() == 2
 
 
 def test_struct_layouts_match_header(rtw):
@@ -27,7 +27,7 @@ def test_struct_layouts_match_header(rtw):
     assert C.sizeof(rtw.Material) == 8 + 3 * 8 * 2 + 16
     assert C.sizeof(rtw.Sphere) == 6 * 8 + 3 * 8 + 8
     assert C.sizeof(rtw.Camera) == 7 * 24 + 24
-    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12
+    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12 + 8
 
 
 def test_cover_scene_equals_oracle_golden(rtw):
@@ -73,6 +73,9 @@ def test_configs_heights(rtw):
     (dict(width=10, height=10, spp=1, row_begin=9, row_stride=2, row_count=2), -1),
     (dict(width=5000, height=5000, spp=1), -2),
     (dict(width=10, height=10, spp=1, precision=7), -1),
+    (dict(width=10, height=10, spp=1, engine=2), -1),
+    (dict(width=10, height=10, spp=1, engine="wavefront", wf_paths=8), -1),
+    (dict(width=10, height=10, spp=1, engine="wavefront", max_depth=70000), -2),
 ])
 def test_render_rejects_bad_params_before_touching_the_gpu(rtw, kw, status):
     sph, mats, _ = rtw.cover_scene(42)
@@ -104,6 +107,20 @@ def test_workspace_bytes(rtw):
     chunks = (500 + 31) // 32
     assert n >= chunks * 1200 * 675 * 3 * 8
     assert n < chunks * 1200 * 675 * 3 * 8 + 4096
+
+
+def test_workspace_bytes_wavefront(rtw):
+    """Wavefront engine: + two SoA path queues, the hit arrays and the home
+    slots (rtw_capi.hip ws_layout), per in-flight path."""
+    base = rtw.workspace_bytes(rtw.make_params(1200, 675, 500))
+    for prec, r in (("f64", 8), ("f32", 4)):
+        for n in (1 << 16, 1 << 20):
+            p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n)
+            per_path = 2 * (10 * r + 8 + 4 + 4) + (r + 4) + (24 + 4 + 4)
+            extra = rtw.workspace_bytes(p) - base
+            assert n * per_path <= extra <= n * per_path + 64 * 256
+    d = rtw.make_params(64, 36, 1, engine="wavefront")
+    assert rtw.workspace_bytes(d) > rtw.DEFAULT_WF_PATHS * 100
 
 
 def test_no_cpu_fallback_without_gpu(rtw):

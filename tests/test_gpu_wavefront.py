@@ -1,0 +1,112 @@
+"""GPU parity of the wavefront engine (BASELINE.json configs[3]: SoA path
+queues in HBM, per-bounce extend/shade kernels, persistent grids).
+
+It computes the same Tier-B image as the megakernel: every sample runs the
+same device functions in the same order and a home slot adds its unit's
+samples in sample order, so the bar is bit-identical output — against the
+oracle (same bar as test_gpu_parity.py) and against the megakernel (every
+byte of rgb and every float of the linear mean).  Queue capacities from 64
+paths (heavy slot recycling, long drain) to more paths than work units.
+"""
+import numpy as np
+import pytest
+
+from helpers import diff_stats, to_oracle_camera, to_oracle_scene
+from test_gpu_parity import ASPECT, assert_parity, custom_scene, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cover(rtw, oracle):
+    sph, mats, _ = rtw.cover_scene(42)
+    cam = rtw.cover_camera(ASPECT)
+    return sph, mats, cam, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam)
+
+
+def both(rtw, cam, sph, mats, **kw):
+    """(megakernel rgb, mean), (wavefront rgb, mean) for the same params."""
+    wf_paths = kw.pop("wf_paths", 0)
+    a = rtw.render(cam, sph, mats, rtw.make_params(**kw), want_mean=True)
+    b = rtw.render(cam, sph, mats, rtw.make_params(engine="wavefront", wf_paths=wf_paths, **kw), want_mean=True)
+    return a, b
+
+
+def assert_identical(a, b, what):
+    (ra, ma), (rb, mb) = a, b
+    assert (ra == rb).all(), (what, diff_stats(ra, rb))
+    assert np.array_equal(ma.view(np.uint32), mb.view(np.uint32)), what
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("w,spp,chunk,paths", [(400, 16, 0, 0), (160, 40, 7, 4096), (96, 3, 0, 64),
+                                              (64, 9, 4, 1 << 16)])
+def test_wavefront_cover_parity(rtw, oracle, cover, precision, w, spp, chunk, paths):
+    sph, mats, cam, osc, ocam = cover
+    h = rtw.image_height(w, ASPECT)
+    kw = dict(width=w, height=h, spp=spp, chunk=chunk, precision=precision)
+    mk, wf = both(rtw, cam, sph, mats, wf_paths=paths, **kw)
+    assert_identical(mk, wf, f"wavefront vs megakernel {precision} {w}x{h}x{spp} paths {paths}")
+    o = oracle_render(oracle, osc, ocam, **kw)
+    assert_parity(wf[0], o, f"wavefront {precision} {w}x{h}x{spp} chunk {chunk} paths {paths}")
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 5])
+def test_wavefront_depth_edges(rtw, oracle, cover, depth):
+    sph, mats, cam, osc, ocam = cover
+    kw = dict(width=64, height=36, spp=4, max_depth=depth)
+    mk, wf = both(rtw, cam, sph, mats, wf_paths=256, **kw)
+    assert_identical(mk, wf, f"depth {depth}")
+    assert_parity(wf[0], oracle_render(oracle, osc, ocam, **kw), f"wavefront depth {depth}")
+    if depth == 0:
+        assert (wf[0] == 0).all()
+
+
+def test_wavefront_empty_scene(rtw, cover):
+    _, _, cam, _, _ = cover
+    a = rtw.render(cam, None, None, rtw.make_params(32, 18, 3))
+    b = rtw.render(cam, None, None, rtw.make_params(32, 18, 3, engine="wavefront", wf_paths=64))
+    assert (a == b).all()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_wavefront_custom_scene(rtw, oracle, precision):
+    sph, mats = custom_scene(rtw)
+    cam = rtw.camera_init((13, 2, 3), (0, 0.5, 0), (0, 1, 0), 30.0, ASPECT, 0.2, 10.0, 0.0, 1.0)
+    kw = dict(width=128, height=72, spp=16, precision=precision, chunk=5)
+    mk, wf = both(rtw, cam, sph, mats, wf_paths=2048, **kw)
+    assert_identical(mk, wf, f"custom {precision}")
+    o = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam), **kw)
+    assert_parity(wf[0], o, f"wavefront custom {precision}")
+
+
+def test_wavefront_row_shards(rtw, cover):
+    sph, mats, cam, _, _ = cover
+    W, H = 120, 68
+    full = rtw.render(cam, sph, mats, rtw.make_params(W, H, 8))
+    for world in (2, 8):
+        for r in (0, world - 1):
+            part = rtw.render(cam, sph, mats, rtw.make_params(W, H, 8, row_begin=r, row_stride=world,
+                                                              engine="wavefront", wf_paths=1000))
+            assert (part == full[r::world]).all(), (world, r)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
+    """configs[1] at full size (1200x675x500): the wavefront frame equals the
+    megakernel frame byte for byte (the megakernel's rows are oracle-checked
+    in test_gpu_parity.py)."""
+    import torch
+    from rtw_amd.device import TorchRenderer
+
+    sph, mats, cam, _, _ = cover
+    R = TorchRenderer(sph, mats, 0)
+    outs = []
+    for eng in ("megakernel", "wavefront"):
+        p = rtw.make_params(1200, 675, 500, precision=precision, engine=eng)
+        rgb = torch.empty((675, 1200, 3), dtype=torch.uint8, device="cuda:0")
+        mean = torch.empty((675, 1200, 3), dtype=torch.float32, device="cuda:0")
+        R.render(cam, p, out=rgb, mean=mean)
+        torch.cuda.synchronize()
+        outs.append((rgb.cpu().numpy(), mean.cpu().numpy()))
+    assert_identical(outs[0], outs[1], f"config2 {precision}")
