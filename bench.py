@@ -18,7 +18,10 @@ rank time.
 
 Extra fields: roofline (dominant kernel = trace; HIP events on the render
 stream), cpu_baseline (oracle Tier A = the reference's algorithm, sequential
-RNG, one core, on a bounded sample of the same frame).
+RNG, one core, on a bounded sample of the same frame), f32_hybrid_variant,
+wavefront_variant (BASELINE configs[3]: the same frame on the wavefront
+engine, bit-identical image, with its HBM roofline).  --engine wavefront makes
+the wavefront engine the headline.
 """
 from __future__ import annotations
 
@@ -233,22 +236,33 @@ def main():
     n_chunks = (spp + chunk - 1) // chunk
     hbm_bytes = rc * W * n_chunks * 24
     hbm_gbs = hbm_bytes / (trace_ms_avg * 1e-3) / 1e9
-    roofline = {
-        "bound": "valu-fp64" if args.precision == "f64" else "valu-fp32",
-        "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
-        "frac": round(achieved_tf / peak, 4),
-        "traffic": traffic_per_launch(args, W, H, spp),
-        "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
-        "flop_per_launch": flops, "segments_per_launch": counts["segments"],
-        "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
-        "note": "megakernel is FP64-VALU + divergence bound; MFMA n/a (no contraction); HBM traffic is "
-                "~24 B per 32 samples by construction (DESIGN.md §Roofline)",
-    }
+    if args.engine == "megakernel":
+        roofline = {
+            "bound": "valu-fp64" if args.precision == "f64" else "valu-fp32",
+            "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved_tf / peak, 4),
+            "traffic": traffic_per_launch(args, W, H, spp),
+            "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
+            "flop_per_launch": flops, "segments_per_launch": counts["segments"],
+            "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
+            "note": "megakernel is FP64-VALU + divergence bound; MFMA n/a (no contraction); HBM traffic is "
+                    "~24 B per 32 samples by construction (DESIGN.md §Roofline)",
+        }
+    else:  # wavefront headline: HBM-bound path queues
+        byts = wavefront_bytes(counts, args.precision, rc * W * n_chunks)
+        gbs = byts / (trace_ms_avg * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
+                    "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,
+                    "valu": {"achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
+                             "frac": round(achieved_tf / peak, 4)}}
 
     extra = {}
     if not args.no_f32_variant and args.precision == "f64":
-        p32 = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc, precision="f32")
+        p32 = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc, precision="f32",
+                            engine=args.engine, wf_paths=args.wf_paths)
         for _ in range(max(1, args.warmup)):
             rend.render(cam, p32, out=out)
         torch.cuda.synchronize()

@@ -163,7 +163,8 @@ int rtw_render_device(rtw_scene scene, const rtw_camera *cam, const rtw_params *
 
 /* Statistics pass (diagnostic, not the product path's timing): counts the
  * bounce segments and sphere tests the same render performs.  counts_out[4] =
- * {samples, segments, static_tests, moving_tests}. Synchronous. */
+ * {samples, segments, static_tests, moving_tests}. Synchronous.  Both engines
+ * count samples and segments (the wavefront engine in its shade kernel). */
 int rtw_render_counts(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                       void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
 

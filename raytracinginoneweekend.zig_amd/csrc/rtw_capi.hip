@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -67,6 +68,13 @@ int blocks_per_cu(int dev, int prec, size_t lds, int var) {
   auto& d = g_dev[dev];
   auto& e = d.bpc[{prec, var}];
   if (e.second == 0 || e.first != lds) e = {lds, rtwk::trace_blocks_per_cu(prec, lds, var)};
+  return e.second;
+}
+// Wavefront bounce kernels: resident workgroups per CU (cached per device).
+int wf_bpc(int dev, int prec, int kernel, size_t lds) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto& e = g_dev[dev].bpc[{prec, -kernel}];
+  if (e.second == 0 || e.first != lds) e = {lds, rtwk::wf_blocks_per_cu(prec, kernel, lds)};
   return e.second;
 }
 // Kernel tuning variant (rtw_trace.hip VAR bits).  Defaults from the in-process
@@ -350,14 +358,19 @@ int validate(const rtw_params* p) {
   return RTW_OK;
 }
 
-uint32_t wf_paths(const rtw_params* p) { return p->wf_paths ? p->wf_paths : RTW_DEFAULT_WF_PATHS; }
+// Wavefront queue capacity: wf_paths rounded up to whole segments (one per wave).
+uint32_t wf_segs(const rtw_params* p) {
+  const uint32_t n = p->wf_paths ? p->wf_paths : RTW_DEFAULT_WF_PATHS;
+  return (n + rtwk::kSegCap - 1) / rtwk::kSegCap;
+}
 
-// Workspace: partial chunk sums | counters (unit queue head, wavefront queue
-// lengths) | stats | wavefront region (engine 1 only, rtw_internal.hpp
-// WfArgs): two path queues, the hit arrays, the home slots.
+// Workspace: partial chunk sums | counters (unit queue head, live-path poll
+// word) | stats | wavefront region (engine 1 only, rtw_internal.hpp WfArgs):
+// two path queues, the hit arrays, the home slots, per-segment counts (x2)
+// and unit reservoirs.
 struct WsLayout {
-  size_t partial_off, partial_bytes, counter_off, count_a_off, count_b_off, stats_off;
-  size_t wf_off, wf_queue_bytes, total;
+  size_t partial_off, partial_bytes, counter_off, live_off, stats_off;
+  size_t wf_off, total;
 };
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk).
@@ -367,16 +380,15 @@ WsLayout ws_layout(const rtw_params* p) {
   w.partial_off = 0;
   w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
   w.counter_off = al256(w.partial_bytes);
-  w.count_a_off = w.counter_off + 64;
-  w.count_b_off = w.counter_off + 128;
+  w.live_off = w.counter_off + 64;
   w.stats_off = w.counter_off + 256;
   w.total = w.stats_off + 256;  // stats: 32 x u64
   w.wf_off = w.total;
-  w.wf_queue_bytes = 0;
   if (p->engine == RTW_ENGINE_WAVEFRONT) {
-    const size_t n = wf_paths(p), r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
-    w.wf_queue_bytes = wf_queue_bytes(n, r);
-    w.total += 2 * w.wf_queue_bytes + al256(n * r) + al256(n * 4) + al256(n * 24) + 2 * al256(n * 4);
+    const size_t segs = wf_segs(p), n = segs * rtwk::kSegCap;
+    const size_t r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
+    w.total += 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * 24) + 2 * al256(n * 4) +
+               2 * al256(segs * 4) + al256(segs * 8);
   }
   return w;
 }
@@ -440,8 +452,8 @@ struct WfLaunch<double> {
   static hipError_t ext(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
     return rtwk::launch_wf_extend_f64(a, g, l, s);
   }
-  static hipError_t shd(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
-    return rtwk::launch_wf_shade_f64(a, g, l, s);
+  static hipError_t shd(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_shade_f64(a, g, l, s, stats);
   }
 };
 template <>
@@ -452,8 +464,8 @@ struct WfLaunch<float> {
   static hipError_t ext(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
     return rtwk::launch_wf_extend_f32(a, g, l, s);
   }
-  static hipError_t shd(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
-    return rtwk::launch_wf_shade_f32(a, g, l, s);
+  static hipError_t shd(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_shade_f32(a, g, l, s, stats);
   }
 };
 
@@ -483,53 +495,56 @@ uint32_t* poll_words() {
 }
 
 // Wavefront render: generate, then batches of kWfIters (extend, shade)
-// pairs; after each batch the live-path count of queue A is copied to pinned
-// memory, and the host stops once a batch (checked one batch behind, so the
-// GPU never idles on the poll) left the queue empty.  Empty batches cost
-// only the launches: every kernel reads its queue length first.
+// pairs; after each batch wf_count sums the segment counts of queue A and the
+// total is copied to pinned memory.  The host stops once a batch (checked one
+// batch behind, so the GPU never idles on the poll) left the queue empty.
+// Empty batches cost only the launches: every wave reads its count first.
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
 int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned char* ws, const WsLayout& L, int dev,
-                  size_t lds, hipStream_t stream) {
+                  size_t lds, hipStream_t stream, bool stats) {
   if (ta.max_depth == 0) {  // rayColor(depth 0) is black (main.zig:105-108): no segment to trace
     HIP_TRY(hipMemsetAsync(ws + L.partial_off, 0, L.partial_bytes, stream));
     return RTW_OK;
   }
-  const size_t n = wf_paths(p);
+  const uint32_t segs = wf_segs(p);
+  const size_t n = (size_t)segs * rtwk::kSegCap;
   rtwk::WfArgs<R> a;
   std::memset(&a, 0, sizeof(a));
   a.t = ta;
   unsigned char* b = ws + L.wf_off;
   const rtwk::PathBuf<R> qa = carve_queue<R>(b, n), qb = carve_queue<R>(b, n);
-  a.hit_t = reinterpret_cast<R*>(b);
-  b += al256(n * sizeof(R));
-  a.hit_k = reinterpret_cast<int32_t*>(b);
-  b += al256(n * 4);
-  a.home_sum = reinterpret_cast<double*>(b);
-  b += al256(n * 24);
-  a.home_unit = reinterpret_cast<uint32_t*>(b);
-  b += al256(n * 4);
-  a.home_s = reinterpret_cast<uint32_t*>(b);
-  a.n_slots = (uint32_t)n;
-  uint32_t* cnt_a = reinterpret_cast<uint32_t*>(ws + L.count_a_off);
-  uint32_t* cnt_b = reinterpret_cast<uint32_t*>(ws + L.count_b_off);
-  const int prec = sizeof(R) == 4 ? 1 : 0;
-  const uint32_t cus = (uint32_t)device_cus(dev);
-  const uint32_t want = (uint32_t)((n + rtwk::kTraceBlock - 1) / rtwk::kTraceBlock);
-  auto grid_of = [&](int k, size_t l) {
-    static thread_local int bpc[2][3] = {{0, 0, 0}, {0, 0, 0}};
-    static thread_local size_t bpc_lds[2][3] = {{0, 0, 0}, {0, 0, 0}};
-    if (bpc[prec][k] == 0 || bpc_lds[prec][k] != l) {
-      bpc[prec][k] = rtwk::wf_blocks_per_cu(prec, k, l);
-      bpc_lds[prec][k] = l;
-    }
-    return std::max(1u, std::min(cus * (uint32_t)bpc[prec][k], want));
+  auto take = [&](size_t bytes) {
+    unsigned char* q = b;
+    b += al256(bytes);
+    return q;
   };
-  const uint32_t g_gen = grid_of(0, 0), g_ext = grid_of(1, lds), g_shd = grid_of(2, lds);
+  a.hit_t = reinterpret_cast<R*>(take(n * sizeof(R)));
+  a.hit_k = reinterpret_cast<int32_t*>(take(n * 4));
+  a.home_sum = reinterpret_cast<double*>(take(n * 24));
+  a.home_unit = reinterpret_cast<uint32_t*>(take(n * 4));
+  a.home_s = reinterpret_cast<uint32_t*>(take(n * 4));
+  uint32_t* seg_a = reinterpret_cast<uint32_t*>(take(segs * 4));
+  uint32_t* seg_b = reinterpret_cast<uint32_t*>(take(segs * 4));
+  a.seg_resv = reinterpret_cast<uint32_t*>(take(segs * 8));
+  a.live = reinterpret_cast<uint32_t*>(ws + L.live_off);
+  a.n_slots = (uint32_t)n;
+  a.n_segs = segs;
+  // Persistent grids: every resident wave slot of each bounce kernel (at most
+  // one wave per segment); the same grids for every launch of the frame.
+  const uint32_t max_grid = (segs + rtwk::kTraceBlock / 64 - 1) / (rtwk::kTraceBlock / 64);
+  // RTW_WF_GRID (development knob): N > 0 = N x the resident grid, capped at one wave per segment.
+  const char* gk = getenv("RTW_WF_GRID");
+  const uint32_t gmul = (gk && *gk) ? (uint32_t)std::max(1, atoi(gk)) : 1u;
+  auto grid_of = [&](int kernel) {
+    const uint32_t per_cu = (uint32_t)wf_bpc(dev, (int)(sizeof(R) == 4), kernel, lds);
+    return std::max(1u, std::min((uint32_t)device_cus(dev) * per_cu * gmul, max_grid));
+  };
+  const uint32_t grid = grid_of(2), grid_ext = grid_of(1);
   // generate -> queue A
   a.out = qa;
-  a.count_out = cnt_a;
-  hipError_t e = WfLaunch<R>::gen(a, g_gen, 0, stream);
+  a.seg_out = seg_a;
+  hipError_t e = WfLaunch<R>::gen(a, grid, 0, stream);
   if (e != hipSuccess) return fail(RTW_EHIP, "wavefront generate launch: %s", hipGetErrorString(e));
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
@@ -539,19 +554,25 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // Termination bound (never reached by a correct kernel): every iteration
   // advances every live path by one segment.
   const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / kWfIters + 4;
+  // Wall-clock guard as well (RTW_WF_TIMEOUT_S, default 300 s): a queue that
+  // never drains is reported instead of hanging the caller.
+  const char* tos = getenv("RTW_WF_TIMEOUT_S");
+  const double timeout_s = (tos && *tos) ? atof(tos) : 300.0;
+  const auto t_start = std::chrono::steady_clock::now();
   int st = RTW_OK;
   for (uint64_t batch = 0;; ++batch) {
     for (int k = 0; k < kWfIters && st == RTW_OK; ++k) {
       const bool even = (k & 1) == 0;
       a.in = even ? qa : qb;
       a.out = even ? qb : qa;
-      a.count_in = even ? cnt_a : cnt_b;
-      a.count_out = even ? cnt_b : cnt_a;
-      if ((e = WfLaunch<R>::ext(a, g_ext, lds, stream)) != hipSuccess ||
-          (e = WfLaunch<R>::shd(a, g_shd, lds, stream)) != hipSuccess)
+      a.seg_in = even ? seg_a : seg_b;
+      a.seg_out = even ? seg_b : seg_a;
+      if ((e = WfLaunch<R>::ext(a, grid_ext, lds, stream)) != hipSuccess ||
+          (e = WfLaunch<R>::shd(a, grid, lds, stream, stats)) != hipSuccess)
         st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
     }
-    if (st == RTW_OK && (hipMemcpyAsync(&poll[batch & 1], cnt_a, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+    if (st == RTW_OK && (rtwk::launch_wf_count(seg_a, segs, a.live, stream) != hipSuccess ||
+                         hipMemcpyAsync(&poll[batch & 1], a.live, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
                          hipEventRecord(ev[batch & 1], stream) != hipSuccess))
       st = fail(RTW_EHIP, "wavefront poll enqueue failed");
     if (st != RTW_OK) break;
@@ -562,14 +583,14 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       }
       if (poll[(batch - 1) & 1] == 0u) break;
     }
-    if (batch > max_batches) {
+    if (batch > max_batches ||
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s) {
       st = fail(RTW_EHIP, "wavefront queue did not drain after %llu batches", (unsigned long long)batch);
       break;
     }
   }
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
-  (void)prec;
   return st;
 }
 
@@ -594,16 +615,16 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   hipError_t e;
   if (timer) HIP_TRY(hipEventRecord(timer->start, stream));
   if (p->engine == RTW_ENGINE_WAVEFRONT) {
-    if (mode != 0) return fail(RTW_UNSUPPORTED, "statistics passes run on the megakernel engine");
+    if (mode == 2) return fail(RTW_UNSUPPORTED, "phase profile runs on the megakernel engine");
     int st;
     if (p->precision == RTW_PRECISION_F32) {
       rtwk::TraceArgs<float> a;
       fill_args(a, sc->v32, cam, p, ws, L);
-      st = run_wavefront<float>(a, p, ws, L, dev, lds, stream);
+      st = run_wavefront<float>(a, p, ws, L, dev, lds, stream, mode == 1);
     } else {
       rtwk::TraceArgs<double> a;
       fill_args(a, sc->v64, cam, p, ws, L);
-      st = run_wavefront<double>(a, p, ws, L, dev, lds, stream);
+      st = run_wavefront<double>(a, p, ws, L, dev, lds, stream, mode == 1);
     }
     if (st != RTW_OK) return st;
     e = hipSuccess;

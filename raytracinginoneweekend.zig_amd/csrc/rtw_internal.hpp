@@ -99,7 +99,13 @@ constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;
 // state, depth and the home slot that owns its (pixel, chunk) unit.  Two
 // queues ping-pong: extend(in) writes the closest hit per queue position,
 // shade(in -> out) scatters, finishes samples, refills units/samples and
-// appends the live paths to `out` compactly (one atomic per wave).
+// appends the live paths to `out`.
+// The queues are cut into SEGMENTS of kSegCap paths, each owned by one
+// persistent wave: a wave always extends / shades its own segments, compacts
+// survivors within a segment (no global atomics), deals units from the
+// segment's reservoir (one global atomic per kWfBatch units), and a segment
+// runs on the same XCD every launch (fixed grid, round-robin dispatch).
+constexpr uint32_t kSegCap = 64;  // paths per segment (one 64-lane wave round)
 template <typename R>
 struct PathBuf {
   R *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz, *tm;
@@ -122,19 +128,23 @@ struct WfArgs {
   double* home_sum; // [slot][3]
   uint32_t* home_unit;
   uint32_t* home_s;
-  uint32_t* count_in;   // live paths in `in`
-  uint32_t* count_out;  // live paths appended to `out` (extend zeroes it)
-  uint32_t n_slots;
-  uint32_t pad;
+  uint32_t* seg_in;    // [segment] live paths in `in`
+  uint32_t* seg_out;   // [segment] live paths written to `out` (shade)
+  uint32_t* seg_resv;  // [segment][2] unit reservoir [next, end)
+  uint32_t* live;      // wf_count: sum of seg_in (host poll word)
+  uint32_t n_slots, n_segs;
 };
 
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
 hipError_t launch_wf_extend_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
-hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
 hipError_t launch_wf_extend_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
-hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
-// Resident workgroups per CU: kernel 0 = generate, 1 = extend, 2 = shade.
+hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+// Resident workgroups per CU of a bounce kernel (1 = extend, 2 = shade): the
+// persistent grid of that kernel is CUs x this.
 int wf_blocks_per_cu(int precision, int kernel, size_t lds);
+// live = sum of seg_in[0..n_segs) (one workgroup).
+hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* live, hipStream_t s);
 
 }  // namespace rtwk

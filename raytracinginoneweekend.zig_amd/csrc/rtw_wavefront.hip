@@ -1,9 +1,12 @@
 // rtw_wavefront.hip — the wavefront engine (BASELINE.json configs[3]): the
 // reference's render loop + rayColor (main.zig:378-402, :103-122) as
-// per-bounce kernels over SoA path queues in HBM, persistent-grid launches.
+// per-bounce kernels over SoA path queues in HBM.
 //
 //   generate : every home slot takes a (pixel, chunk) unit and starts its
 //              first sample (Camera.getRay, main.zig:91-100) -> queue A
+// A wave owns fixed queue segments of kSegCap paths for the whole frame
+// (rtw_internal.hpp): compaction is wave-local, units come from a per-segment
+// reservoir, and a segment stays on one XCD (fixed grid, persistent waves).
 //   extend   : closest hit (HittableList.hit, hittable.zig:231-244) for every
 //              path of the input queue -> (hit root, winner) per position
 //   shade    : background on a miss (main.zig:109-112) or Material.scatter
@@ -11,7 +14,7 @@
 //              f64 chunk sum, a finished chunk publishes it and the slot takes
 //              the next unit; the slot's next sample starts at once, so the
 //              queue stays full until the units run out.  Live paths are
-//              appended to the output queue (one atomic per wave, coalesced).
+//              appended, in order, to the wave's segment of the output queue.
 //
 // Arithmetic: the same device functions as the megakernel (rtw_device.hpp),
 // so every sample is bit-identical to the megakernel and the Tier-B oracle;
@@ -25,6 +28,8 @@
 #include "rtw_device.hpp"
 
 namespace rtwk {
+
+constexpr uint32_t kWfBatch = 64;  // units per reservoir refill (one global atomic)
 
 static_assert(offsetof(WfArgs<double>, t) == 0 && offsetof(WfArgs<float>, t) == 0,
               "kargs<R>() reads TraceArgs at kernarg offset 0");
@@ -69,21 +74,30 @@ __device__ __forceinline__ bool decode_unit(const TraceArgs<R>& A, uint32_t unit
   return px < A.W && ly < A.row_count;  // else a padding unit of an edge tile
 }
 
-// Lanes with `need` take units from the device queue (wave-converged; one
-// atomic per wave per round).  On return `got` lanes own `unit`; lanes that
-// found the queue exhausted have need == false and got == false.
+// Lanes with `need` take units from the wave's reservoir [qnext, qend)
+// (wave-uniform), refilled kWfBatch units at a time from the device queue —
+// the megakernel's dealing (rtw_trace.hip step 1) with smaller batches, so
+// little work sits in reservoirs when the queue runs dry.  Wave-converged.  On return
+// `got` lanes own `unit`; lanes that found the queue exhausted do not.
 template <typename R>
-__device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, bool need, uint32_t lid, uint32_t& unit) {
+__device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, bool need, uint32_t lid, uint32_t& qnext,
+                                          uint32_t& qend, uint32_t& unit) {
   bool got = false;
   for (;;) {
     const uint64_t m = __ballot(need);
     if (!m) break;
     const uint32_t n = (uint32_t)__popcll(m);
-    uint32_t b = 0;
-    if (lid == 0) b = atomicAdd(A.counter, n);
-    b = __shfl(b, 0);
+    const uint32_t rank = mbcnt64(m);
+    const uint32_t rem = qend - qnext;
+    const uint32_t grab = max(kWfBatch, n - rem);  // (used only when n > rem)
+    uint32_t base2 = 0;
+    if (n > rem) {
+      uint32_t b = 0;
+      if (lid == 0) b = atomicAdd(A.counter, grab);
+      base2 = __shfl(b, 0);
+    }
     if (need) {
-      const uint32_t u = b + mbcnt64(m);
+      const uint32_t u = rank < rem ? qnext + rank : base2 + (rank - rem);
       uint32_t px, ly, c;
       if (u >= A.total_units) {
         need = false;  // queue exhausted: the slot retires
@@ -92,6 +106,12 @@ __device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, bool need, uint
         got = true;
         unit = u;
       }
+    }
+    if (n > rem) {
+      qnext = base2 + (n - rem);
+      qend = base2 + grab;
+    } else {
+      qnext += n;
     }
   }
   return got;
@@ -117,16 +137,14 @@ __device__ __forceinline__ void start_path(const TraceArgs<R>& A, uint32_t unit,
   start_sample_ray<R>(kargs<R>(), L, u, v, dk[0], dk[1]);
 }
 
-// Append the wave's live lanes to queue `out` (positions contiguous per wave).
+// Append the wave's live lanes to its own segment of queue `out` at
+// positions out_n, out_n+1, ... (order kept; no atomics).
 template <typename R>
-__device__ __forceinline__ void push_path(const WfArgs<R>& A, bool live, uint32_t lid, const Lane<R>& L,
-                                          uint32_t slot) {
+__device__ __forceinline__ void push_path(const PathBuf<R>& out, uint32_t seg_base, uint32_t& out_n, bool live,
+                                          const Lane<R>& L, uint32_t slot) {
   const uint64_t m = __ballot(live);
-  if (!m) return;
-  uint32_t b = 0;
-  if (lid == 0) b = atomicAdd(A.count_out, (uint32_t)__popcll(m));
-  b = __shfl(b, 0);
-  if (live) store_path(A.out, b + mbcnt64(m), L, slot);
+  if (live) store_path(out, seg_base + out_n + mbcnt64(m), L, slot);
+  out_n += (uint32_t)__popcll(m);
 }
 
 template <typename R>
@@ -134,27 +152,49 @@ __device__ __forceinline__ uint32_t chunk_end(const TraceArgs<R>& A, uint32_t c)
   return min(c * A.chunk + A.chunk, A.spp);
 }
 
+// Waves are persistent over segments: wave w owns segments w, w + nwaves, ...
+// for the whole frame (the host launches the same grid every time).
+__device__ __forceinline__ uint32_t wave_id() { return blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint32_t wave_count() { return gridDim.x * (kTraceBlock / 64); }
+
+// Workgroup-uniform: does any segment of this workgroup's waves hold paths?
+// (Drain phase: most workgroups skip the LDS staging and exit.)
+template <typename R>
+__device__ __forceinline__ bool group_has_work(const WfArgs<R>& A) {
+  bool work = false;
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) work |= A.seg_in[seg] != 0u;
+  return __syncthreads_or(work) != 0;
+}
+
 // ---------------------------------------------------------------- generate --
+// Every slot of the wave's segments takes a unit and starts its first sample.
 template <typename R, bool F32>
 __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
   const uint32_t lid = lane_id();
-  const uint32_t wave = (blockIdx.x * kTraceBlock + threadIdx.x) >> 6;
-  const uint32_t nwaves = gridDim.x * (kTraceBlock / 64);
-  for (uint32_t base = wave * 64; base < A.n_slots; base += nwaves * 64) {  // wave-uniform
-    const uint32_t slot = base + lid;
-    uint32_t unit = 0;
-    const bool got = take_unit(A.t, slot < A.n_slots, lid, unit);
-    Lane<R> L{};
-    if (got) {
-      uint32_t px, ly, c;
-      decode_unit(A.t, unit, px, ly, c);
-      const uint32_t s = c * A.t.chunk;
-      A.home_unit[slot] = unit;
-      A.home_s[slot] = s;
-      A.home_sum[3 * slot] = A.home_sum[3 * slot + 1] = A.home_sum[3 * slot + 2] = 0.0;
-      start_path(A.t, unit, s, L);
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+    const uint32_t base = seg * kSegCap;
+    uint32_t qnext = 0, qend = 0, out_n = 0;
+    for (uint32_t k = 0; k < kSegCap; k += 64) {
+      const uint32_t slot = base + k + lid;
+      uint32_t unit = 0;
+      const bool got = take_unit(A.t, true, lid, qnext, qend, unit);
+      Lane<R> L{};
+      if (got) {
+        uint32_t px, ly, c;
+        decode_unit(A.t, unit, px, ly, c);
+        const uint32_t s = c * A.t.chunk;
+        A.home_unit[slot] = unit;
+        A.home_s[slot] = s;
+        A.home_sum[3 * (size_t)slot] = A.home_sum[3 * (size_t)slot + 1] = A.home_sum[3 * (size_t)slot + 2] = 0.0;
+        start_path(A.t, unit, s, L);
+      }
+      push_path(A.out, base, out_n, got, L, slot);
     }
-    push_path(A, got, lid, L, slot);
+    if (lid == 0) {
+      A.seg_out[seg] = out_n;
+      A.seg_resv[2 * seg] = qnext;
+      A.seg_resv[2 * seg + 1] = qend;
+    }
   }
 }
 
@@ -162,41 +202,71 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
 template <typename R, bool F32>
 __global__ void __launch_bounds__(kTraceBlock) wf_extend(WfArgs<R> A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
+  if (!group_has_work(A)) return;
   const SceneView<R> S = A.t.sc;
   const LdsTables<R> T = stage_tables<R>(S, lds_raw);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *A.count_out = 0u;  // shade appends to it next
-  const uint32_t n_in = *A.count_in;
   const uint32_t lid = lane_id();
   const R tmin = A.t.tmin, pre_k = A.t.pre_k;
   KStats st;
-  for (uint32_t i = blockIdx.x * kTraceBlock + threadIdx.x; i < n_in; i += gridDim.x * kTraceBlock) {
-    Lane<R> L;
-    L.o = mk(A.in.ox[i], A.in.oy[i], A.in.oz[i]);
-    L.d = mk(A.in.dx[i], A.in.dy[i], A.in.dz[i]);
-    L.time = A.in.tm[i];
-    L.skip = F32 ? (int)(A.in.dsk[i] >> 16) - 1 : -1;
-    int hit = -1;
-    R tmax = (R)__builtin_huge_val();
-    closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
-    A.hit_t[i] = tmax;
-    A.hit_k[i] = hit;
+  // Software-pipelined over the wave's segments: the next segment's ray is
+  // loaded while this one's closest hit runs.
+  auto load = [&](uint32_t seg, Lane<R>& L, bool& ok) {
+    ok = seg < A.n_segs && lid < A.seg_in[seg];
+    if (ok) {
+      const uint32_t i = seg * kSegCap + lid;
+      L.o = mk(A.in.ox[i], A.in.oy[i], A.in.oz[i]);
+      L.d = mk(A.in.dx[i], A.in.dy[i], A.in.dz[i]);
+      L.time = A.in.tm[i];
+      L.skip = F32 ? (int)(A.in.dsk[i] >> 16) - 1 : -1;
+    }
+  };
+  static_assert(kSegCap == 64, "one path per lane per segment");
+  Lane<R> cur;
+  bool cur_ok;
+  load(wave_id(), cur, cur_ok);
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+    Lane<R> nxt;
+    bool nxt_ok;
+    load(seg + wave_count(), nxt, nxt_ok);
+    if (cur_ok) {
+      int hit = -1;
+      R tmax = (R)__builtin_huge_val();
+      closest_hit<R, F32, 0, 0>(S, T, cur, tmin, pre_k, lid, st, hit, tmax);
+      const uint32_t i = seg * kSegCap + lid;
+      A.hit_t[i] = tmax;
+      A.hit_k[i] = hit;
+    }
+    cur = nxt;
+    cur_ok = nxt_ok;
   }
 }
 
 // ------------------------------------------------------------------- shade --
-template <typename R, bool F32>
+// STATS: count finished samples and shaded segments (rtw_render_counts) —
+// with the megakernel's counts they prove every sample ran exactly once.
+template <typename R, bool F32, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
+  const uint32_t lid = lane_id();
+  if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
+    if (lid == 0)
+      for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) A.seg_out[seg] = 0u;
+    return;
+  }
   const SceneView<R> S = A.t.sc;
   const LdsTables<R> T = stage_tables<R>(S, lds_raw);
-  const uint32_t n_in = *A.count_in;
-  const uint32_t lid = lane_id();
-  const uint32_t wave = (blockIdx.x * kTraceBlock + threadIdx.x) >> 6;
-  const uint32_t nwaves = gridDim.x * (kTraceBlock / 64);
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+  const uint32_t n_in = A.seg_in[seg];
+  if (n_in == 0u) {
+    if (lid == 0) A.seg_out[seg] = 0u;
+    continue;
+  }
+  const uint32_t base = seg * kSegCap;
   const uint32_t npix = A.t.row_count * A.t.W;
-  for (uint32_t base = wave * 64; base < n_in; base += nwaves * 64) {  // wave-uniform: coop_reject converged
-    const uint32_t i = base + lid;
-    const bool valid = i < n_in;
+  uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
+  for (uint32_t k = 0; k < n_in; k += 64) {  // wave-uniform: coop_reject runs converged
+    const uint32_t i = base + k + lid;
+    const bool valid = k + lid < n_in;
     Lane<R> L{};
     L.skip = -1;
     uint32_t slot = 0;
@@ -256,7 +326,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
         need_sample = true;
       }
     }
-    if (take_unit(A.t, need_unit, lid, unit)) {
+    if (take_unit(A.t, need_unit, lid, qnext, qend, unit)) {
       uint32_t px, ly, c;
       decode_unit(A.t, unit, px, ly, c);
       s = c * A.t.chunk;
@@ -267,8 +337,40 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
       need_sample = true;
     }
     if (need_sample) start_path(A.t, unit, s, L);
-    push_path(A, valid && (!ended || need_sample), lid, L, slot);
+    push_path(A.out, base, out_n, valid && (!ended || need_sample), L, slot);
+    if constexpr (STATS) {
+      const uint32_t ns = (uint32_t)__popcll(__ballot(ended)), nv = (uint32_t)__popcll(__ballot(valid));
+      if (lid == 0) {
+        atomicAdd(A.t.stats + 0, (unsigned long long)ns);
+        atomicAdd(A.t.stats + 1, (unsigned long long)nv);
+      }
+    }
   }
+  if (lid == 0) {
+    A.seg_out[seg] = out_n;
+    A.seg_resv[2 * seg] = qnext;
+    A.seg_resv[2 * seg + 1] = qend;
+  }
+  }
+}
+
+// Live paths of a queue = sum of its segment counts (the host's poll word).
+__global__ void __launch_bounds__(1024) wf_count(const uint32_t* seg, uint32_t n, uint32_t* live) {
+  __shared__ uint32_t part[16];
+  uint32_t s = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) s += seg[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    *live = t;
+  }
+}
+hipError_t launch_wf_count(const uint32_t* seg, uint32_t n, uint32_t* live, hipStream_t s) {
+  hipLaunchKernelGGL(wf_count, dim3(1), dim3(1024), 0, s, seg, n, live);
+  return hipGetLastError();
 }
 
 // ----------------------------------------------------------------- launch --
@@ -278,8 +380,10 @@ static hipError_t launch3(int k, const WfArgs<R>& a, uint32_t grid, size_t lds, 
     hipLaunchKernelGGL((wf_generate<R, F32>), dim3(grid), dim3(kTraceBlock), 0, s, a);
   else if (k == 1)
     hipLaunchKernelGGL((wf_extend<R, F32>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 2)
+    hipLaunchKernelGGL((wf_shade<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else
-    hipLaunchKernelGGL((wf_shade<R, F32>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+    hipLaunchKernelGGL((wf_shade<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
@@ -288,8 +392,8 @@ hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t g, size_t l,
 hipError_t launch_wf_extend_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<double, false>(1, a, g, l, s);
 }
-hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
-  return launch3<double, false>(2, a, g, l, s);
+hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<double, false>(stats ? 3 : 2, a, g, l, s);
 }
 hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<float, true>(0, a, g, l, s);
@@ -297,24 +401,20 @@ hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t g, size_t l, 
 hipError_t launch_wf_extend_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<float, true>(1, a, g, l, s);
 }
-hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
-  return launch3<float, true>(2, a, g, l, s);
+hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<float, true>(stats ? 3 : 2, a, g, l, s);
 }
 
 template <typename R, bool F32>
-static int occ3(int k, size_t lds) {
-  int nb = 0;
-  hipError_t e;
-  if (k == 0)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_generate<R, F32>, kTraceBlock, 0);
-  else if (k == 1)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_extend<R, F32>, kTraceBlock, lds);
-  else
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wf_shade<R, F32>, kTraceBlock, lds);
-  return (e == hipSuccess && nb > 0) ? nb : 1;
+static int occ_wf(int kernel, size_t lds) {
+  int n = 0;
+  const hipError_t e = kernel == 1
+                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_extend<R, F32>, kTraceBlock, lds)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shade<R, F32, false>, kTraceBlock, lds);
+  return (e == hipSuccess && n > 0) ? n : 1;
 }
 int wf_blocks_per_cu(int precision, int kernel, size_t lds) {
-  return precision == 1 ? occ3<float, true>(kernel, lds) : occ3<double, false>(kernel, lds);
+  return precision == 1 ? occ_wf<float, true>(kernel, lds) : occ_wf<double, false>(kernel, lds);
 }
 
 }  // namespace rtwk

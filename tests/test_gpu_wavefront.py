@@ -110,3 +110,23 @@ def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
         torch.cuda.synchronize()
         outs.append((rgb.cpu().numpy(), mean.cpu().numpy()))
     assert_identical(outs[0], outs[1], f"config2 {precision}")
+
+
+@pytest.mark.parametrize("w,spp,paths", [(400, 128, 360_000), (1200, 64, 0), (160, 40, 64)])
+def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths):
+    """Statistics pass: the wavefront shades exactly W*H*spp samples and the
+    megakernel's number of bounce segments.  Duplicated or lost units would
+    leave the image bits unchanged (a unit's samples are deterministic) but
+    change these counts.  (400x225x128 at 360k paths: more segments than
+    resident waves, so waves own several segments.)"""
+    import torch
+    from rtw_amd.device import TorchRenderer
+
+    sph, mats, cam, _, _ = cover
+    h = rtw.image_height(w, ASPECT)
+    R = TorchRenderer(sph, mats, 0)
+    mk = R.counts(cam, rtw.make_params(w, h, spp))
+    wf = R.counts(cam, rtw.make_params(w, h, spp, engine="wavefront", wf_paths=paths))
+    torch.cuda.synchronize()
+    assert mk["samples"] == w * h * spp
+    assert (wf["samples"], wf["segments"]) == (mk["samples"], mk["segments"])
