@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
+#define RTW_ABI_VERSION 3
 
 typedef enum {
   RTW_OK = 0,
@@ -167,6 +167,123 @@ int rtw_render_device(rtw_scene scene, const rtw_camera *cam, const rtw_params *
  * count samples and segments (the wavefront engine in its shade kernel). */
 int rtw_render_counts(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                       void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
+
+/* =================================================== general worlds ===
+ * Every other scene of the reference (main.zig:123-290) and BASELINE.json
+ * configs[4] (globe + 10k spheres): the full Hittable / Material / Texture
+ * vocabulary, flattened.  Nested lists (Box = 6 rects) become consecutive
+ * primitives in list order; Translate / RotateY wrappers become a transform
+ * chain per primitive.  Rendered by the world kernel (f64, BVH traversal),
+ * whose per-sample contract is oracle/rtw_world.h Tier B. */
+
+typedef enum {
+  RTW_PRIM_SPHERE = 0,        /* Sphere        hittable.zig:90-155  a = c[3], c[3], r, 0, 0 */
+  RTW_PRIM_MOVING_SPHERE = 1, /* MovingSphere  hittable.zig:157-226 a = c0[3], c1[3], r, t0, t1 */
+  RTW_PRIM_XY_RECT = 2,       /* XyRect        hittable.zig:270-323 a = x0, x1, y0, y1, k */
+  RTW_PRIM_XZ_RECT = 3,       /* XzRect        hittable.zig:325-378 a = x0, x1, z0, z1, k */
+  RTW_PRIM_YZ_RECT = 4        /* YzRect        hittable.zig:380-427 a = y0, y1, z0, z1, k */
+} rtw_prim_kind;
+
+typedef struct {
+  uint32_t kind, mat;
+  int32_t xform;              /* index into xforms, -1 = none */
+  uint32_t reserved;
+  double a[9];
+} rtw_prim;
+
+#define RTW_MAX_XFORM_OPS 4
+typedef enum {
+  RTW_XF_TRANSLATE = 0,       /* Translate hittable.zig:472-503: v = offset */
+  RTW_XF_ROTATE_Y = 1         /* RotateY   hittable.zig:505-608: v = {sin_t, cos_t, angle} */
+} rtw_xform_op;
+typedef struct {              /* op[0] is the OUTERMOST wrapper */
+  uint32_t n;
+  uint32_t op[RTW_MAX_XFORM_OPS];
+  double v[RTW_MAX_XFORM_OPS][3];
+} rtw_xform;
+
+typedef enum {
+  RTW_TEX_SOLID = 0,          /* texture.zig:46-55 */
+  RTW_TEX_CHECKER = 1,        /* texture.zig:57-83 (solid odd / even) */
+  RTW_TEX_NOISE = 2,          /* texture.zig:85-105 (perlin index, scale) */
+  RTW_TEX_IMAGE = 3           /* texture.zig:107-144 (image index) */
+} rtw_texture_kind;
+typedef struct {
+  uint32_t kind, perlin, image, reserved;
+  double color[3], odd[3], even[3];
+  double scale;
+} rtw_texture;
+
+typedef enum {
+  RTW_WMAT_LAMBERT = 0,       /* DiffuseMaterial      material.zig:41-53 (albedo texture) */
+  RTW_WMAT_METAL = 1,         /* MetalMaterial        material.zig:55-66 */
+  RTW_WMAT_DIELECTRIC = 2,    /* DielectricMaterial   material.zig:68-92 */
+  RTW_WMAT_LIGHT = 3          /* DiffuseLightMaterial material.zig:94-110 (emit texture) */
+} rtw_wmaterial_kind;
+typedef struct {
+  uint32_t kind, tex;
+  double albedo[3];
+  double fuzz, ir;
+} rtw_wmaterial;
+
+typedef struct {              /* Perlin, perlin.zig:10-40 */
+  double ranvec[256][3];
+  uint32_t perm[3][256];
+} rtw_perlin;
+
+typedef struct {              /* decoded texture image: RGBA8, row-major, top row first */
+  uint32_t width, height;
+  const uint8_t *rgba;
+} rtw_image;
+
+typedef struct {
+  const rtw_prim *prims;          uint32_t n_prims;
+  const rtw_xform *xforms;        uint32_t n_xforms;
+  const rtw_texture *textures;    uint32_t n_textures;
+  const rtw_wmaterial *mats;      uint32_t n_mats;
+  const rtw_perlin *perlins;      uint32_t n_perlins;
+  const rtw_image *images;        uint32_t n_images;
+} rtw_world_desc;
+
+/* Camera / image settings a scene sets in main() (main.zig:303-376). */
+typedef struct {
+  double look_from[3], look_at[3], vfov, aperture, aspect;
+  double background[3];
+  uint32_t width, height, spp, reserved;
+} rtw_scene_settings;
+
+/* Scene builders of main.zig on DefaultPrng.init(seed): 1 cover (:157),
+ * 2 two spheres (:123), 3 two Perlin spheres (:140), 4 earth (:223),
+ * 5 simple light (:235), 6 Cornell box (:256), 7 globe + 10k random spheres
+ * (configs[4]; not a reference scene).  `image` is the earth texture
+ * (scenes 4, 7; pixels are copied).  The built scene owns its arrays;
+ * rtw_built_scene_desc points into them until rtw_built_scene_free. */
+typedef struct rtw_built_scene_s *rtw_built_scene;
+int rtw_build_scene(uint32_t scene_id, uint64_t seed, const rtw_image *image, rtw_built_scene *out);
+int rtw_built_scene_desc(rtw_built_scene b, rtw_world_desc *desc, rtw_scene_settings *settings,
+                         uint64_t rng_state_after[4]);
+int rtw_built_scene_free(rtw_built_scene b);
+
+/* Upload a world to the CURRENT device: tables + a BVH (flags bit 0 =
+ * RTW_WORLD_LINEAR: no BVH, test every primitive). */
+#define RTW_WORLD_LINEAR 1u
+typedef struct rtw_world_s *rtw_world;
+int rtw_world_create(const rtw_world_desc *desc, uint32_t flags, rtw_world *out);
+int rtw_world_destroy(rtw_world world);
+/* BVH statistics: nodes, leaves, max depth, max leaf size. */
+int rtw_world_bvh_info(rtw_world world, uint32_t info_out[4]);
+
+/* Asynchronous render of a world (params.precision must be F64, engine
+ * MEGAKERNEL); workspace sized by rtw_workspace_bytes(params). */
+int rtw_world_render_device(rtw_world world, const rtw_camera *cam, const rtw_params *params,
+                            void *workspace, size_t workspace_bytes, uint8_t *d_rgb, float *d_mean,
+                            void *stream, rtw_timer timer);
+/* Synchronous host-buffer render of a world description. */
+int rtw_world_render(const rtw_camera *cam, const rtw_world_desc *desc, const rtw_params *params,
+                     uint8_t *rgb_out, float *mean_out);
+/* Statistics pass: counts_out[4] = {samples, segments, node_visits, prim_tests}. */
+int rtw_world_render_counts(rtw_world world, const rtw_camera *cam, const rtw_params *params,
+                            void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
 
 #ifdef __cplusplus
 }

@@ -242,3 +242,179 @@ def write_ppm(path: str, img: np.ndarray):
     with open(path, "wb") as f:
         f.write(b"P6\n%d %d\n255\n" % (w, h))
         f.write(np.ascontiguousarray(img, np.uint8).tobytes())
+
+
+# ------------------------------------------------------ general worlds ----
+# rtw_world.h: flattened Hittable/Material/Texture/Perlin worlds (scenes 1-7).
+RW_SPHERE, RW_MOVING, RW_XY, RW_XZ, RW_YZ = 0, 1, 2, 3, 4
+RW_XF_TRANSLATE, RW_XF_ROTATE_Y = 0, 1
+RW_TEX_SOLID, RW_TEX_CHECKER, RW_TEX_NOISE, RW_TEX_IMAGE = 0, 1, 2, 3
+RW_LAMBERT, RW_METAL, RW_DIELECTRIC, RW_LIGHT = 0, 1, 2, 3
+
+
+class WPrim(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("mat", C.c_uint32), ("xform", C.c_int32), ("pad", C.c_uint32),
+                ("a", C.c_double * 9)]
+
+
+class WXform(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("op", C.c_uint32 * 4), ("v", (C.c_double * 3) * 4)]
+
+
+class WTexture(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("perlin", C.c_uint32), ("image", C.c_uint32), ("pad", C.c_uint32),
+                ("color", C.c_double * 3), ("odd", C.c_double * 3), ("even", C.c_double * 3),
+                ("scale", C.c_double)]
+
+
+class WMaterial(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("tex", C.c_uint32), ("albedo", C.c_double * 3), ("fuzz", C.c_double),
+                ("ir", C.c_double)]
+
+
+class WPerlin(C.Structure):
+    _fields_ = [("ranvec", (C.c_double * 3) * 256), ("perm", (C.c_uint32 * 256) * 3)]
+
+
+class WImage(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgba", C.c_void_p)]
+
+
+class World(C.Structure):
+    _fields_ = [("n_prims", C.c_uint32), ("n_xforms", C.c_uint32), ("n_textures", C.c_uint32),
+                ("n_mats", C.c_uint32), ("n_perlins", C.c_uint32), ("n_images", C.c_uint32),
+                ("prims", C.POINTER(WPrim)), ("xforms", C.POINTER(WXform)), ("textures", C.POINTER(WTexture)),
+                ("mats", C.POINTER(WMaterial)), ("perlins", C.POINTER(WPerlin)), ("images", C.POINTER(WImage)),
+                ("look_from", C.c_double * 3), ("look_at", C.c_double * 3), ("vfov", C.c_double),
+                ("aperture", C.c_double), ("aspect", C.c_double), ("background", C.c_double * 3),
+                ("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32)]
+
+
+def _world_lib():
+    L = lib()
+    if getattr(L, "_world_ready", False):
+        return L
+    P = C.POINTER
+    L.rw_scene.restype = P(World)
+    L.rw_scene.argtypes = [C.c_uint32, U64x4, P(WImage)]
+    L.rw_world_free.argtypes = [P(World)]
+    L.rw_int_range_less_than_u64.restype = C.c_uint64
+    L.rw_int_range_less_than_u64.argtypes = [U64x4, C.c_uint64, C.c_uint64]
+    L.rw_perlin_noise.restype = C.c_double
+    L.rw_perlin_noise.argtypes = [P(WPerlin), C.c_double * 3]
+    L.rw_perlin_turb.restype = C.c_double
+    L.rw_perlin_turb.argtypes = [P(WPerlin), C.c_double * 3, C.c_uint32]
+    L.rw_texture_value.argtypes = [P(World), C.c_uint32, C.c_double, C.c_double, C.c_double * 3, C.c_double * 3]
+    L.rw_sphere_uv.argtypes = [C.c_double * 3, P(C.c_double), P(C.c_double)]
+    for n in ("rw_sin", "rw_cos", "rw_acos"):
+        getattr(L, n).restype = C.c_double
+        getattr(L, n).argtypes = [C.c_double]
+    L.rw_atan2.restype = C.c_double
+    L.rw_atan2.argtypes = [C.c_double, C.c_double]
+    L.rw_hit.restype = C.c_int
+    L.rw_hit.argtypes = [P(World), C.c_double * 3, C.c_double * 3, C.c_double, C.c_double, C.c_double,
+                         P(C.c_double), C.c_double * 3, C.c_double * 3, C.c_double * 2, P(C.c_int)]
+    L.rw_render_tier_a.argtypes = [P(World), P(Camera), C.c_double * 3, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, U64x4, C.c_void_p, C.c_void_p, P(Stats)]
+    L.rw_render_tier_b.argtypes = [P(World), P(Camera), P(Params), C.c_void_p, C.c_void_p, P(Stats)]
+    L._world_ready = True
+    return L
+
+
+class OracleWorld:
+    """A world built by the oracle's scene builders (rw_scene).  Keeps the
+    image buffer alive; frees the C world on close/GC."""
+
+    def __init__(self, scene_id: int, seed: int = 42, image: np.ndarray | None = None,
+                 rng: "ZigRandom | None" = None):
+        L = _world_lib()
+        self.rng = rng if rng is not None else ZigRandom(seed)
+        self._img = None
+        wi = None
+        if image is not None:
+            self._img = np.ascontiguousarray(image, np.uint8)
+            h, w, _ = self._img.shape
+            wi = WImage(w, h, self._img.ctypes.data)
+        self.ptr = L.rw_scene(scene_id, self.rng.s, C.byref(wi) if wi is not None else None)
+        if not self.ptr:
+            raise ValueError(f"unknown scene {scene_id}")
+        self.w = self.ptr.contents
+        self.scene_id = scene_id
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            _world_lib().rw_world_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def camera(self, aspect: float | None = None) -> Camera:
+        """Camera.init with the scene's settings (main.zig:316-376)."""
+        cam = Camera()
+        arr = C.c_double * 3
+        w = self.w
+        lib().ro_camera_init(C.byref(cam), arr(*w.look_from), arr(*w.look_at), arr(0, 1, 0), w.vfov,
+                             aspect if aspect is not None else w.aspect, w.aperture, 10.0, 0.0, 1.0)
+        return cam
+
+    @property
+    def background(self):
+        return tuple(self.w.background)
+
+    def table(self) -> dict:
+        """Plain-python dump (compared with the product's scene builders)."""
+        w = self.w
+        prims = [{"kind": p.kind, "mat": p.mat, "xform": p.xform, "a": list(p.a)}
+                 for p in (w.prims[i] for i in range(w.n_prims))]
+        xfs = [{"n": x.n, "op": list(x.op)[:x.n], "v": [list(x.v[k]) for k in range(x.n)]}
+               for x in (w.xforms[i] for i in range(w.n_xforms))]
+        texs = [{"kind": t.kind, "perlin": t.perlin, "image": t.image, "color": list(t.color), "odd": list(t.odd),
+                 "even": list(t.even), "scale": t.scale} for t in (w.textures[i] for i in range(w.n_textures))]
+        mats = [{"kind": m.kind, "tex": m.tex, "albedo": list(m.albedo), "fuzz": m.fuzz, "ir": m.ir}
+                for m in (w.mats[i] for i in range(w.n_mats))]
+        perl = [{"ranvec": [list(p.ranvec[k]) for k in range(256)], "perm": [list(p.perm[a]) for a in range(3)]}
+                for p in (w.perlins[i] for i in range(w.n_perlins))]
+        return {"prims": prims, "xforms": xfs, "textures": texs, "materials": mats, "perlins": perl,
+                "settings": {"look_from": list(w.look_from), "look_at": list(w.look_at), "vfov": w.vfov,
+                             "aperture": w.aperture, "aspect": w.aspect, "background": list(w.background),
+                             "width": w.width, "height": w.height, "spp": w.spp}}
+
+    def render_tier_a(self, cam: Camera, width: int, height: int, spp: int, depth: int = 50, bg=None):
+        """Tier A over this world, continuing self.rng (the reference's stream)."""
+        out = np.zeros((height, width, 3), np.uint8)
+        st = Stats()
+        _world_lib().rw_render_tier_a(self.ptr, C.byref(cam), (C.c_double * 3)(*(bg or self.background)), width,
+                                      height, spp, depth, self.rng.s, out.ctypes.data, None, C.byref(st))
+        return out, st.as_dict()
+
+    def render_tier_b(self, cam: Camera, width: int, height: int, spp: int, depth: int = 50, seed: int = 42,
+                      bg=None, row_begin: int = 0, row_stride: int = 1, row_count: int | None = None,
+                      chunk: int = 0, threads: int = 0, want_mean=False):
+        if row_count is None:
+            row_count = (height - row_begin + row_stride - 1) // row_stride
+        p = Params(width, height, spp, depth, seed, (C.c_double * 3)(*(bg or self.background)), row_begin,
+                   row_stride, row_count, chunk, 0, threads)
+        out = np.zeros((row_count, width, 3), np.uint8)
+        mean = np.zeros((row_count, width, 3), np.float32) if want_mean else None
+        st = Stats()
+        _world_lib().rw_render_tier_b(self.ptr, C.byref(cam), C.byref(p), out.ctypes.data,
+                                      mean.ctypes.data if want_mean else None, C.byref(st))
+        return (out, mean, st.as_dict()) if want_mean else (out, st.as_dict())
+
+    def hit(self, o, d, time=0.0, t_min=0.001, t_max=float("inf")):
+        arr = C.c_double * 3
+        t = C.c_double()
+        p, n, uv, fr = arr(), arr(), (C.c_double * 2)(), C.c_int()
+        k = _world_lib().rw_hit(self.ptr, arr(*o), arr(*d), time, t_min, t_max, C.byref(t), p, n, uv, C.byref(fr))
+        if k < 0:
+            return None
+        return {"prim": k, "t": t.value, "p": list(p), "normal": list(n), "uv": list(uv), "front": bool(fr.value)}
+
+
+def libm(name: str):
+    """The Tier-B transcendental (ro_libm.h) as a Python callable."""
+    return getattr(_world_lib(), "rw_" + name)

@@ -788,3 +788,39 @@ int rtw_render(const rtw_camera* cam, const rtw_sphere* spheres, uint32_t n, con
 }
 
 }  // extern "C"
+
+// ---- helpers shared with the world path (rtw_world_capi.hip) ----
+int rtw_fail(int status, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return fail(status, "%s", buf);
+}
+int rtw_validate_params(const rtw_params* p) { return validate(p); }
+size_t rtw_ws_total(const rtw_params* p) { return ws_layout(p).total; }
+size_t rtw_ws_stats_off(const rtw_params* p) { return ws_layout(p).stats_off; }
+size_t rtw_ws_counter_off(const rtw_params* p) { return ws_layout(p).counter_off; }
+int rtw_device_cus(int dev) { return device_cus(dev); }
+void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, const rtw_params* p, unsigned char* ws) {
+  fill_args(a, rtwk::SceneView<double>{}, cam, p, ws, ws_layout(p));
+}
+int rtw_launch_finalize(const rtw_params* p, unsigned char* ws, uint8_t* d_rgb, float* d_mean, hipStream_t s) {
+  const WsLayout L = ws_layout(p);
+  rtwk::FinalizeArgs f;
+  f.partial = reinterpret_cast<const double*>(ws + L.partial_off);
+  f.rgb = d_rgb;
+  f.mean = d_mean;
+  f.npix = p->row_count * p->width;
+  f.n_chunks = n_chunks(p);
+  f.scale = 1.0 / (double)p->spp;
+  const hipError_t e = rtwk::launch_finalize(f, s);
+  if (e != hipSuccess) return fail(RTW_EHIP, "finalize kernel launch: %s", hipGetErrorString(e));
+  return RTW_OK;
+}
+int rtw_timer_mark(rtw_timer t, hipStream_t s, bool start) {
+  if (hipEventRecord(start ? t->start : t->stop, s) != hipSuccess) return fail(RTW_EHIP, "timer event record failed");
+  if (!start) t->recorded = true;
+  return RTW_OK;
+}

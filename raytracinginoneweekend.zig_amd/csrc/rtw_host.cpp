@@ -231,10 +231,12 @@ static rtw_material flat_material(const Material& m) {
       if (m.albedo.kind == Texture::Kind::solid) {
         r.kind = RTW_LAMBERT_SOLID;
         put3(r.albedo, m.albedo.color);
-      } else {
+      } else if (m.albedo.kind == Texture::Kind::checker) {
         r.kind = RTW_LAMBERT_CHECKER;
         put3(r.albedo, m.albedo.even);
         put3(r.albedo_odd, m.albedo.odd);
+      } else {
+        r.kind = RTW_DIFFUSE_LIGHT;  // noise / image: not on the cover path (rtw_world_* renders them)
       }
       break;
     case Material::Kind::metal:
@@ -258,6 +260,8 @@ static void flatten_into(const Hittable& h, FlatScene& out, std::map<const Mater
     for (const auto& o : h.objects) flatten_into(o, out, ids);
     return;
   }
+  if (h.kind != Hittable::Kind::sphere && h.kind != Hittable::Kind::movingSphere)
+    throw Error(RTW_UNSUPPORTED, "the cover-scene path renders spheres only (use flattenWorld / rtw_world_*)");
   if (!h.material) throw Error(RTW_EINVAL, "hittable without material");
   auto it = ids.find(h.material.get());
   uint32_t mid;

@@ -6,11 +6,14 @@
 //   rtw::Vec3 / Point3 / Color      src/rtw/vec.zig:8-109
 //   rtw::Random (DefaultPrng)       std.Random.DefaultPrng, used at main.zig:300
 //   rtw::rand helpers               src/rtw/rand.zig:1-40
-//   rtw::Texture                    src/rtw/texture.zig:10-83 (solid, checker)
-//   rtw::Material                   src/rtw/material.zig:16-92
-//   rtw::Hittable                   src/rtw/hittable.zig:22-268 (sphere, movingSphere, list)
+//   rtw::Texture                    src/rtw/texture.zig:10-144 (solid, checker, noise, image)
+//   rtw::Perlin                     src/rtw/perlin.zig:10-124
+//   rtw::Material                   src/rtw/material.zig:16-110
+//   rtw::Hittable                   src/rtw/hittable.zig:22-608 (sphere, movingSphere, list,
+//                                   xy/xz/yzRect, box, translate, rotateY)
 //   rtw::Camera                     src/main.zig:40-101
-//   rtw::generateRandomScene        src/main.zig:157-221
+//   rtw::generate*                  src/main.zig:123-290 (scenes 1-6) + the configs[4] globe
+//                                   scene (rtw_world_host.cpp)
 //   rtw::render                     replaces src/main.zig:378-402 via rtw_render()
 // Zig error unions map to rtw::Error exceptions on the C++ side only; nothing
 // crosses the C ABI except status codes.
@@ -65,35 +68,66 @@ double randomReal(Random& rng, double min, double max);    // rand.zig:18-20
 Vec3 random01(Random& rng);                                // vec.zig:82-88
 Vec3 randomVec(Random& rng, double min, double max);       // vec.zig:90-96
 
+// Random.intRangeLessThan for u64 (Zig std, Lemire; rand.zig:8-10).
+uint64_t randomIntLessThan(Random& rng, uint64_t at_least, uint64_t less_than);
+
+struct Perlin {  // perlin.zig:10-124
+  Vec3 ranvec[256];
+  uint32_t perm[3][256];
+  static std::shared_ptr<Perlin> init(Random& rng);  // perlin.zig:18-40
+};
+
+struct Image {  // zigimg Image, decoded to RGBA8 (texture.zig:107-118)
+  uint32_t width = 0, height = 0;
+  std::vector<uint8_t> rgba;
+};
+
 struct Texture {
-  enum class Kind { solid, checker } kind = Kind::solid;
+  enum class Kind { solid, checker, noise, image } kind = Kind::solid;
   Color color;      // solid
   Color odd, even;  // checker (texture.zig:57-83)
+  std::shared_ptr<Perlin> perlin;  // noise (texture.zig:85-105)
+  double scale = 1;
+  std::shared_ptr<Image> image;    // image (texture.zig:107-144)
   static Texture makeSolid(Color c);
-  static Texture makeChecker(Color odd, Color even);  // texture.zig:17-23
+  static Texture makeChecker(Color odd, Color even);        // texture.zig:17-23
+  static Texture makeNoise(double scale, Random& rng);      // texture.zig:28-30
+  static Texture makeImage(std::shared_ptr<Image> image);   // texture.zig:32-34
 };
 
 struct Material {
   enum class Kind { diffuse, metal, dielectric, diffuse_light } kind = Kind::diffuse;
-  Texture albedo;      // diffuse
+  Texture albedo;      // diffuse albedo / diffuse_light emit
   Color metal_albedo;  // metal
   double fuzz = 0;     // metal
   double ir = 1;       // dielectric
   static std::shared_ptr<Material> diffuse(Texture t);
   static std::shared_ptr<Material> metal(Color albedo, double fuzz);
   static std::shared_ptr<Material> dielectric(double ir);
+  static std::shared_ptr<Material> diffuseLight(Texture emit);  // material.zig:94-110
 };
 
 struct Hittable {
-  enum class Kind { sphere, movingSphere, list } kind = Kind::list;
+  enum class Kind { sphere, movingSphere, list, xyRect, xzRect, yzRect, box, translate, rotateY } kind = Kind::list;
   Point3 center0, center1;
   double time0 = 0, time1 = 1, radius = 0;
+  double a0 = 0, a1 = 0, b0 = 0, b1 = 0, k = 0;  // rects (first, second in-plane axis; plane offset)
+  Point3 box_min, box_max;                       // box (sides in `objects`)
+  Vec3 offset;                                   // translate
+  double sin_t = 0, cos_t = 1, angle = 0;        // rotateY
+  std::shared_ptr<Hittable> object;              // translate / rotateY: Rc(Hittable)
   std::shared_ptr<Material> material;  // Rc(Material) (src/rc.zig)
-  std::vector<Hittable> objects;       // list
+  std::vector<Hittable> objects;       // list, box sides
   static Hittable makeSphere(Point3 c, double r, std::shared_ptr<Material> m);  // main.zig:26-34
   static Hittable makeMovingSphere(Point3 c0, Point3 c1, double t0, double t1, double r,
                                    std::shared_ptr<Material> m);
   static Hittable makeList(std::vector<Hittable> objs);
+  static Hittable makeXyRect(double x0, double x1, double y0, double y1, double k, std::shared_ptr<Material> m);
+  static Hittable makeXzRect(double x0, double x1, double z0, double z1, double k, std::shared_ptr<Material> m);
+  static Hittable makeYzRect(double y0, double y1, double z0, double z1, double k, std::shared_ptr<Material> m);
+  static Hittable makeBox(Point3 p0, Point3 p1, std::shared_ptr<Material> m);             // hittable.zig:34-36
+  static Hittable makeTranslate(std::shared_ptr<Hittable> obj, Vec3 offset);            // hittable.zig:38-40
+  static Hittable makeRotateY(std::shared_ptr<Hittable> obj, double angle_rad);         // hittable.zig:42-44
 };
 
 struct Camera {  // main.zig:40-101
@@ -107,6 +141,28 @@ struct Camera {  // main.zig:40-101
 
 // main.zig:157-221
 Hittable generateRandomScene(Random& rng);
+// main.zig:123-155, :223-290, and the configs[4] globe scene (rtw_world_host.cpp)
+Hittable generateTwoSpheres(Random& rng);
+Hittable generateTwoPerlinSpheres(Random& rng);
+Hittable generateEarthScene(std::shared_ptr<Image> earth);
+Hittable generateSimpleLightScene(Random& rng);
+Hittable generateCornellBox();
+Hittable generateGlobeScene(Random& rng, std::shared_ptr<Image> earth);
+
+// The general world -> flat arrays of the world ABI (rtw_world_desc).
+struct FlatWorld {
+  std::vector<rtw_prim> prims;
+  std::vector<rtw_xform> xforms;
+  std::vector<rtw_texture> textures;
+  std::vector<rtw_wmaterial> materials;
+  std::vector<rtw_perlin> perlins;
+  std::vector<std::shared_ptr<Image>> images;
+  std::vector<rtw_image> image_views;
+  rtw_world_desc desc() const;
+};
+FlatWorld flattenWorld(const Hittable& world);
+// Scene settings of main() (main.zig:303-376) for scene ids 1-7.
+rtw_scene_settings sceneSettings(uint32_t scene_id);
 
 // The world -> flat arrays of the C ABI (Rc(Material) pointers -> indices).
 struct FlatScene {

@@ -147,4 +147,49 @@ int wf_blocks_per_cu(int precision, int kernel, size_t lds);
 // live = sum of seg_in[0..n_segs) (one workgroup).
 hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* live, hipStream_t s);
 
+// ---------------------------------------------------------- world engine --
+// rtw_world.hip / rtw_world_capi.hip: the general-world kernel (all scenes
+// of main.zig, BASELINE.json configs[4]).  f64 tables in HBM, 16 doubles
+// (128 B) per record:
+//   prim   : sphere  {c0.xyz, dc.xyz = c1 - c0, r, t0, t1 - t0, r*r, -, -, -, -, meta(2 x u32 x 2)}
+//            rect    {a0, a1, b0, b1, k, a1 - a0, b1 - b0, ...,                  meta}
+//            meta = {kind | xform+1 << 8, mat, orig list index, -} in doubles 14-15
+//   xform  : {u32 n | op_i << (8 + 4 i)}, v[i].xyz at doubles 4 + 3i
+//   texture: {u32 kind, perlin, image, -}, color, odd, even, scale at doubles 2, 5, 8, 11
+//   material (8 doubles): {u32 kind, tex}, albedo, fuzz, ir at 1, 4, 5
+//   perlin : ranvec 256 x 3 f64, then perm 3 x 256 u32 (per perlin)
+//   image  : {width, height, byte offset} + one RGBA8 byte pool
+//   node   : BVH2 with both child boxes in the parent: lo0.xyz, hi0.xyz, lo1.xyz,
+//            hi1.xyz, {u32 ref0, ref1}; ref bit 31 = leaf {first (bits 0-22), count (23-30)}
+// Prims are stored in BVH leaf order; `orig` keeps the list index for the
+// reference's tie rule (later object wins).
+constexpr uint32_t kWorldRec = 16;
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kBvhStack = 32;  // per-lane LDS stack entries (the builder caps the depth)
+constexpr uint32_t kMaxLeafPrims = 4;
+
+struct WorldView {
+  const double* prim;
+  const double* xform;
+  const double* tex;
+  const double* mat;
+  const double* perlin;
+  const uint32_t* image;   // n_images x {width, height, offset_lo, offset_hi}
+  const uint8_t* pixels;
+  const double* node;
+  uint32_t n_prims, n_nodes, n_perlins, pad;
+};
+
+struct WorldArgs {
+  TraceArgs<double> t;  // MUST stay at offset 0 (kargs<double>()); t.sc unused
+  WorldView w;
+  double margin;        // BVH test widening (rtw_world_capi.hip bvh_margin)
+  unsigned long long* counts;  // stats pass: {samples, segments, node visits, prim tests}
+};
+
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode);
+int world_blocks_per_cu(size_t lds);
+constexpr int kWorldBlock = 256;
+size_t world_lds_bytes(uint32_t n_perlins);
+
 }  // namespace rtwk

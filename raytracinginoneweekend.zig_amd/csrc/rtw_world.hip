@@ -1,0 +1,503 @@
+// rtw_world.hip — the general-world kernel: the reference's render loop and
+// rayColor (main.zig:378-402, :103-122, emission included) over the full
+// Hittable vocabulary (hittable.zig:22-608: spheres, moving spheres, xy/xz/yz
+// rects, boxes, Translate, RotateY), all materials (material.zig:16-121,
+// DiffuseLight included) and textures (texture.zig:10-144: solid, checker,
+// Perlin noise, image), for every scene of main.zig and BASELINE.json
+// configs[4] (globe + 10k spheres).  f64, the reference's arithmetic.
+//
+// Closest hit: BVH2 traversal (both child boxes in the parent node) with a
+// per-lane stack in LDS (kBvhStack entries per lane, column-interleaved so
+// the 64 lanes of a wave hit 64 distinct banks), or a wave-uniform linear
+// loop for small worlds.  The reference's HittableList.hit picks the object of
+// minimal effective root, ties to the later object — an order-independent
+// rule — so visiting primitives in BVH order returns the
+// same winner as long as no box that could hold a winner is pruned: every
+// box test is widened by `margin` (rtw_world_capi.hip bvh_margin: > the
+// largest deviation of a computed root from the exact intersection) and is
+// inclusive at tmax.  A NaN root (the reference's acceptance is then order
+// dependent) sends the lane through the literal sequential loop.
+//
+// Per lane: the megakernel's work units (pixel, chunk of samples) with
+// lane-level regeneration; per sample: the Tier-B counter RNG, rayColor
+// evaluated forward (rad += T * emitted at a light, rad += T * background on a
+// miss).  oracle/rtw_world.h Tier B is the written contract.
+#include <hip/hip_runtime.h>
+
+#include "rtw_device.hpp"
+#include "rtw_libm.hpp"
+
+namespace rtwk {
+
+using D = double;
+using V = V3<D>;
+
+__device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
+
+// Translate / RotateY chains (hittable.zig:478-491, :561-600), op 0 outermost.
+__device__ __forceinline__ void to_object(const D* xf, V& o, V& d) {
+  const uint32_t h = *reinterpret_cast<const uint32_t*>(xf);
+  const uint32_t n = h & 0xFFu;
+  for (uint32_t i = 0; i < n; ++i) {
+    const D* v = xf + 4 + 3 * i;
+    if (((h >> (8 + 4 * i)) & 0xFu) == 0u) {
+      o = sub(o, ld3(v));
+    } else {
+      const D sn = v[0], cs = v[1];
+      const V o0 = o, d0 = d;
+      o.x = cs * o0.x - sn * o0.z;
+      o.z = sn * o0.x + cs * o0.z;
+      d.x = cs * d0.x - sn * d0.z;
+      d.z = sn * d0.x + cs * d0.z;
+    }
+  }
+}
+__device__ __forceinline__ void to_world(const D* xf, V& p, V& nrm) {
+  const uint32_t h = *reinterpret_cast<const uint32_t*>(xf);
+  for (int i = (int)(h & 0xFFu) - 1; i >= 0; --i) {
+    const D* v = xf + 4 + 3 * i;
+    if (((h >> (8 + 4 * i)) & 0xFu) == 0u) {
+      p = add(p, ld3(v));
+    } else {
+      const D sn = v[0], cs = v[1];
+      const V p0 = p, n0 = nrm;
+      p.x = cs * p0.x + sn * p0.z;
+      p.z = -sn * p0.x + cs * p0.z;
+      nrm.x = cs * n0.x + sn * n0.z;
+      nrm.z = -sn * n0.x + cs * n0.z;
+    }
+  }
+}
+
+// The primitive's effective root for ray (o, d) in world space: Sphere.hit /
+// MovingSphere.hit root selection (hittable.zig:96-116, :166-187) or the rect
+// plane hit with its containment test (:278-286, :333-341, :388-396).
+// Returns false when the primitive cannot be hit at t >= tmin; t may be NaN.
+__device__ __forceinline__ bool prim_root(const WorldView& W, const D* r, V o, V d, D time, D tmin, D& t) {
+  const uint32_t* m = meta_of(r);
+  const uint32_t kind = m[0] & 0xFFu;
+  const int xf = (int)(m[0] >> 8) - 1;
+  if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+  if (kind <= 1u) {
+    V c = ld3(r);
+    if (kind == 1u) c = add(c, mul(ld3(r + 3), (time - r[7]) / r[8]));  // hittable.zig:219-221
+    const V oc = sub(o, c);
+    const D a = norm2(d);
+    const D hb = dot(oc, d);
+    const D cc = norm2(oc) - r[9];
+    const D disc = hb * hb - a * cc;
+    if (disc < 0.0) return false;
+    const D sq = sqrt(disc);
+    D root = (-hb - sq) / a;
+    if (root < tmin) root = (-hb + sq) / a;
+    t = root;
+    return !(root < tmin);
+  }
+  D ok, oa, ob, dk, da, db;
+  if (kind == 2u) {
+    ok = o.z, oa = o.x, ob = o.y, dk = d.z, da = d.x, db = d.y;
+  } else if (kind == 3u) {
+    ok = o.y, oa = o.x, ob = o.z, dk = d.y, da = d.x, db = d.z;
+  } else {
+    ok = o.x, oa = o.y, ob = o.z, dk = d.x, da = d.y, db = d.z;
+  }
+  const D tt = (r[4] - ok) / dk;
+  if (tt < tmin) return false;
+  const D x = oa + tt * da, y = ob + tt * db;
+  if (x < r[0] || x > r[1] || y < r[2] || y > r[3]) return false;
+  t = tt;
+  return true;
+}
+
+struct WHit {
+  int pos;     // stored position of the winner (-1: miss)
+  int orig;    // its list index
+  D t;
+  bool nan;
+};
+__device__ __forceinline__ void accept(WHit& h, D t, int pos, int orig, D tmin) {
+  if (t != t) h.nan = true;
+  if (!(t < tmin) & ((t < h.t) | ((t == h.t) & (orig > h.orig)))) {
+    h.t = t;
+    h.pos = pos;
+    h.orig = orig;
+  }
+}
+
+// The reference's literal sequential loop (HittableList.hit, :231-244) over
+// the list in its original order; `order` maps list index -> stored position.
+__device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* order, V o, V d, D time, D tmin,
+                                        WHit& h) {
+  h.pos = -1;
+  h.orig = -1;
+  h.t = (D)__builtin_huge_val();
+  for (uint32_t i = 0; i < W.n_prims; ++i) {
+    const uint32_t k = order[i];
+    const D* r = W.prim + kWorldRec * k;
+    D t;
+    if (!prim_root(W, r, o, d, time, tmin, t)) continue;
+    if (h.t < t) continue;  // `t_max < root` rejects; NaN roots are accepted (as in the reference)
+    h.t = t;
+    h.pos = (int)k;
+    h.orig = (int)i;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack, const V& o, const V& d, D time,
+                                        D tmin, WHit& h, unsigned long long& nv, unsigned long long& nt) {
+  h.pos = -1;
+  h.orig = -1;
+  h.t = (D)__builtin_huge_val();
+  h.nan = false;
+  if (W.n_nodes == 0) {  // linear: wave-uniform loop, scalar-loaded records
+    for (uint32_t k = 0; k < W.n_prims; ++k) {
+      const D* r = W.prim + kWorldRec * k;
+      D t;
+      if (MODE == 1) ++nt;
+      if (prim_root(W, r, o, d, time, tmin, t)) accept(h, t, (int)k, (int)meta_of(r)[2], tmin);
+    }
+    return;
+  }
+  const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
+  uint32_t sp = 0, node = 0;
+  auto leaf = [&](uint32_t ref) {
+    const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & 0xFFu;
+    for (uint32_t k = first; k < first + cnt; ++k) {
+      const D* r = W.prim + kWorldRec * k;
+      D t;
+      if (MODE == 1) ++nt;
+      if (prim_root(W, r, o, d, time, tmin, t)) accept(h, t, (int)k, (int)meta_of(r)[2], tmin);
+    }
+  };
+  for (;;) {
+    if (MODE == 1) ++nv;
+    const D* nd = W.node + kWorldRec * node;
+    const uint32_t* refs = reinterpret_cast<const uint32_t*>(nd + 12);
+    D tn[2];
+    bool hit[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {  // widened slab test, inclusive at the current closest root
+      const D* b = nd + 6 * c;
+      const D x0 = ((b[0] - m) - o.x) * inv.x, x1 = ((b[3] + m) - o.x) * inv.x;
+      const D y0 = ((b[1] - m) - o.y) * inv.y, y1 = ((b[4] + m) - o.y) * inv.y;
+      const D z0 = ((b[2] - m) - o.z) * inv.z, z1 = ((b[5] + m) - o.z) * inv.z;
+      const D n = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), tmin));
+      const D f = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), h.t));
+      tn[c] = n;
+      hit[c] = n <= f;
+    }
+    const uint32_t r0 = refs[0], r1 = refs[1];
+    if (hit[0] && (r0 & kLeafBit)) leaf(r0);
+    if (hit[1] && (r1 & kLeafBit)) leaf(r1);
+    const bool i0 = hit[0] && !(r0 & kLeafBit), i1 = hit[1] && !(r1 & kLeafBit);
+    if (i0 && i1) {
+      const bool first0 = tn[0] <= tn[1];
+      stack[(sp++) * kWorldBlock] = first0 ? r1 : r0;
+      node = first0 ? r0 : r1;
+    } else if (i0) {
+      node = r0;
+    } else if (i1) {
+      node = r1;
+    } else {
+      if (sp == 0) break;
+      node = stack[(--sp) * kWorldBlock];
+    }
+  }
+}
+
+// Texture.value (texture.zig:36-144) for the winner's record.
+__device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v, V p) {
+  const D* t = W.tex + kWorldRec * ti;
+  const uint32_t* th = reinterpret_cast<const uint32_t*>(t);
+  switch (th[0]) {
+    case 1u:  // checker: only the sign of sin(10x) sin(10y) sin(10z) matters (rtw_math.hpp)
+      return rtwm::checker_odd((D)10 * p.x, (D)10 * p.y, (D)10 * p.z) ? ld3(t + 5) : ld3(t + 8);
+    case 2u: {  // noise, texture.zig:101-105 + Perlin.turb/noise (perlin.zig:49-91)
+      const D* pr = W.perlin + (size_t)th[1] * (256 * 3 + 384);
+      const uint32_t* perm = reinterpret_cast<const uint32_t*>(pr + 256 * 3);
+      D accum = 0.0, weight = 1.0;
+      V q = p;
+      for (int oct = 0; oct < 7; ++oct) {
+        const D fx = floor(q.x), fy = floor(q.y), fz = floor(q.z);
+        const D uu0 = q.x - fx, vv0 = q.y - fy, ww0 = q.z - fz;
+        const D uu = uu0 * uu0 * (3 - 2 * uu0), vv = vv0 * vv0 * (3 - 2 * vv0), ww = ww0 * ww0 * (3 - 2 * ww0);
+        const int i = (int)fx, j = (int)fy, k = (int)fz;
+        D nz = 0.0;
+        for (int di = 0; di < 2; ++di)
+          for (int dj = 0; dj < 2; ++dj)
+            for (int dk = 0; dk < 2; ++dk) {
+              const uint32_t ix = (uint32_t)(i + di) & 255u, iy = (uint32_t)(j + dj) & 255u,
+                             iz = (uint32_t)(k + dk) & 255u;
+              const D* c = pr + 3 * (perm[ix] ^ perm[256 + iy] ^ perm[512 + iz]);
+              const D ti = (D)di, tj = (D)dj, tk = (D)dk;
+              const V wgt = mk(uu - ti, vv - tj, ww - tk);
+              nz += (ti * uu + (1.0 - ti) * (1.0 - uu)) * (tj * vv + (1.0 - tj) * (1.0 - vv)) *
+                    (tk * ww + (1.0 - tk) * (1.0 - ww)) * dot(ld3(c), wgt);
+            }
+        accum += weight * nz;
+        weight *= 0.5;
+        q = mk(q.x * 2.0, q.y * 2.0, q.z * 2.0);
+      }
+      const D kk = 0.5 * (1.0 + rtwl::sin(t[11] * p.z + 10.0 * fabs(accum)));
+      return mk(1 * kk, 1 * kk, 1 * kk);
+    }
+    case 3u: {  // image, texture.zig:121-144 (row clamp: rtw_world.h)
+      const uint32_t* im = W.image + 4 * th[2];
+      const uint32_t w = im[0], hgt = im[1];
+      const D uc = fmax(0.0, fmin(u, 1.0));
+      const D vc = 1.0 - fmax(0.0, fmin(v, 1.0));
+      const uint64_t i = (uint64_t)(uc * (D)w), j = (uint64_t)(vc * (D)hgt);
+      const uint64_t i_ = i < w - 1 ? i : w - 1;
+      uint64_t j_ = j < w - 1 ? j : w - 1;
+      if (j_ > hgt - 1) j_ = hgt - 1;
+      const uint8_t* px = W.pixels + ((uint64_t)im[2] | ((uint64_t)im[3] << 32)) + (j_ * w + i_) * 4;
+      const uchar4 c = *reinterpret_cast<const uchar4*>(px);
+      if (c.w == 0) return mk(0.0, 0.0, 1.0);
+      const D s = 1.0 / 255.0;
+      return mk(s * (D)c.x, s * (D)c.y, s * (D)c.z);
+    }
+    default:
+      return ld3(t + 2);
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kWorldBlock) world_kernel(WorldArgs A) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + threadIdx.x;
+  const WorldView W = A.w;  // a local copy: no reference to the by-value argument escapes
+  const D margin = A.margin;
+  const uint32_t* order = reinterpret_cast<const uint32_t*>(W.node + kWorldRec * W.n_nodes);
+  const uint32_t lid = lane_id();
+  const uint32_t npix = A.t.row_count * A.t.W;
+  const uint32_t units_per_tile = kTileW * kTileH * A.t.n_chunks;
+  const D tmin = A.t.tmin;
+  Lane<D> L;
+  L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
+  L.sx = L.sy = L.sz = 0.0;
+  L.rs = 0;
+  L.skip = -1;
+  V rad = mk(0.0, 0.0, 0.0);
+  bool have_unit = false, have_ray = false, done = false;
+  uint32_t qnext = 0, qend = 0;
+  unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0;
+  for (;;) {
+    // ---- take units (wave-uniform; rtw_trace.hip step 1) ----
+    const bool need = !have_unit && !done;
+    const uint64_t needmask = __ballot(need);
+    if (needmask) {
+      const uint32_t n = (uint32_t)__popcll(needmask);
+      const uint32_t rank = mbcnt64(needmask);
+      const uint32_t rem = qend - qnext;
+      uint32_t base2 = 0;
+      if (n > rem) {
+        uint32_t b = 0;
+        if (lid == 0) b = atomicAdd(A.t.counter, kBatch);
+        base2 = __shfl(b, 0);
+      }
+      if (need) {
+        const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
+        if (unit >= A.t.total_units) {
+          done = true;
+        } else {
+          const uint32_t tile = unit / units_per_tile;
+          const uint32_t r = unit - tile * units_per_tile;
+          const uint32_t ty = tile / A.t.tiles_x, tx = tile - ty * A.t.tiles_x;
+          const uint32_t px = tx * kTileW + ((r & 63u) & 7u), ly = ty * kTileH + ((r & 63u) >> 3);
+          if (px < A.t.W && ly < A.t.row_count) {
+            have_unit = true;
+            L.px = px;
+            L.ly = ly;
+            L.c = r >> 6;
+            L.s = L.c * A.t.chunk;
+            L.s_end = min(L.s + A.t.chunk, A.t.spp);
+            L.sx = L.sy = L.sz = 0.0;
+          }
+        }
+      }
+      if (n > rem) {
+        qnext = base2 + (n - rem);
+        qend = base2 + kBatch;
+      } else {
+        qnext += n;
+      }
+    }
+    if (!__any(have_unit)) {
+      if (__all(done)) break;
+      continue;
+    }
+    // ---- new sample ----
+    if (have_unit && !have_ray) {
+      D u, v, dk[2];
+      start_sample_uv<D>(kargs<D>(), L, u, v);
+      for (;;) {  // randomPointInUnitDisk, rand.zig:30-36
+        dk[0] = rrange_m11<D>(L.rs);
+        dk[1] = rrange_m11<D>(L.rs);
+        if (in_unit_ball<D, 2>(dk)) break;
+      }
+      start_sample_ray<D>(kargs<D>(), L, u, v, dk[0], dk[1]);
+      rad = mk(0.0, 0.0, 0.0);
+      have_ray = true;
+    }
+    // ---- one segment ----
+    bool ended = false;
+    if (have_ray) {
+      if (L.depth == A.t.max_depth) {
+        ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
+      } else {
+        if (MODE == 1) ++n_segments;
+        WHit h;
+        closest<MODE>(W, margin, stack, L.o, L.d, L.time, tmin, h, n_visits, n_tests);
+        if (__builtin_expect(h.nan, 0)) seq_hit(W, order, L.o, L.d, L.time, tmin, h);
+        if (h.pos < 0) {  // miss: background (main.zig:109-112)
+          rad = add(rad, mulv(L.T, ld3(opaque(kargs<D>())->bg)));
+          ended = true;
+        } else {
+          // Hit record of the winner (object space, then the wrappers back).
+          const D* r = W.prim + kWorldRec * h.pos;
+          const uint32_t* mt = meta_of(r);
+          const uint32_t kind = mt[0] & 0xFFu;
+          const int xf = (int)(mt[0] >> 8) - 1;
+          V o = L.o, d = L.d;
+          if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+          V p = add(o, mul(d, h.t)), nrm;
+          bool front;
+          D tu = 0.0, tv = 0.0;
+          const D* mp = W.mat + 8 * mt[1];
+          const uint32_t* mh = reinterpret_cast<const uint32_t*>(mp);
+          const uint32_t mkind = mh[0], mtex = mh[1];
+          const bool image_tex =
+              (mkind == 0u || mkind == 3u) && *reinterpret_cast<const uint32_t*>(W.tex + kWorldRec * mtex) == 3u;
+          if (kind <= 1u) {
+            V c = ld3(r);
+            if (kind == 1u) c = add(c, mul(ld3(r + 3), (L.time - r[7]) / r[8]));
+            const V outward = divs(sub(p, c), r[6]);
+            front = dot(outward, d) < 0.0;
+            nrm = front ? outward : mul(outward, -1.0);
+            if (kind == 0u && image_tex) {  // getSphereUv (hittable.zig:145-150)
+              const D pi = 3.14159265358979323846;
+              tu = (rtwl::atan2(-outward.z, outward.x) + pi) / (2.0 * pi);
+              tv = rtwl::acos(-outward.y) / pi;
+            }
+          } else {
+            D oa, ob, da, db;
+            V n0;
+            if (kind == 2u) {
+              oa = o.x, ob = o.y, da = d.x, db = d.y, n0 = mk(0.0, 0.0, 1.0);
+            } else if (kind == 3u) {
+              oa = o.x, ob = o.z, da = d.x, db = d.z, n0 = mk(0.0, 1.0, 0.0);
+            } else {
+              oa = o.y, ob = o.z, da = d.y, db = d.z, n0 = mk(1.0, 0.0, 0.0);
+            }
+            tu = (oa + h.t * da - r[0]) / r[5];
+            tv = (ob + h.t * db - r[2]) / r[6];
+            front = dot(n0, d) < 0.0;
+            nrm = front ? n0 : mul(n0, -1.0);
+          }
+          if (xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
+          if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
+            rad = add(rad, mulv(L.T, tex_value(W, mtex, tu, tv, p)));
+            ended = true;
+          } else {
+            V ndir, att;
+            bool absorbed = false;
+            if (mkind == 0u) {  // Lambertian (material.zig:44-52)
+              D b3[3];
+              for (;;) {  // randomPointInUnitSphere, rand.zig:22-28
+                b3[0] = rrange_m11<D>(L.rs);
+                b3[1] = rrange_m11<D>(L.rs);
+                b3[2] = rrange_m11<D>(L.rs);
+                if (in_unit_ball<D, 3>(b3)) break;
+              }
+              ndir = add(nrm, normalized(mk(b3[0], b3[1], b3[2])));
+              if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
+              att = tex_value(W, mtex, tu, tv, p);
+            } else if (mkind == 1u) {  // Metal (material.zig:59-65)
+              const V ud = normalized(L.d);
+              const V refl = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
+              D b3[3];
+              for (;;) {
+                b3[0] = rrange_m11<D>(L.rs);
+                b3[1] = rrange_m11<D>(L.rs);
+                b3[2] = rrange_m11<D>(L.rs);
+                if (in_unit_ball<D, 3>(b3)) break;
+              }
+              ndir = add(refl, mul(mk(b3[0], b3[1], b3[2]), mp[4]));
+              att = ld3(mp + 1);
+              absorbed = !(dot(refl, nrm) > 0.0);
+            } else {  // Dielectric (material.zig:72-91)
+              const D ir = mp[5];
+              const D ratio = front ? 1.0 / ir : ir;
+              const V ud = normalized(L.d);
+              const D cos_t = fmin(dot(mul(ud, -1.0), nrm), 1.0);
+              const D sin_t = sqrt(1.0 - cos_t * cos_t);
+              bool refr = false;
+              if (ratio * sin_t <= 1.0) {
+                const D r0 = (1.0 - ratio) / (1.0 + ratio);
+                const D r1 = r0 * r0;
+                const D x = 1.0 - cos_t, x2 = x * x;
+                refr = r1 + (1.0 - r1) * (x * (x2 * x2)) < rnd<D>(L.rs);  // Zig pow(x, 5.0)
+              }
+              if (refr) {
+                const D ct = fmin(dot(mul(ud, -1.0), nrm), 1.0);
+                const V perp = mul(add(ud, mul(nrm, ct)), ratio);
+                ndir = add(perp, mul(nrm, -sqrt(fabs(1.0 - norm2(perp)))));
+              } else {
+                ndir = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
+              }
+              att = mk(1.0, 1.0, 1.0);
+            }
+            if (absorbed) {
+              ended = true;
+            } else {
+              L.T = mulv(L.T, att);
+              L.o = p;
+              L.d = ndir;
+              L.depth++;
+            }
+          }
+        }
+      }
+    }
+    if (ended) {  // the sample's radiance joins its chunk sum (main.zig:393)
+      L.sx += rad.x;
+      L.sy += rad.y;
+      L.sz += rad.z;
+      L.s++;
+      have_ray = false;
+      if (MODE == 1) ++n_samples;
+      if (L.s == L.s_end) {
+        double* dst = A.t.partial + ((size_t)L.c * npix + (size_t)L.ly * A.t.W + L.px) * 3;
+        dst[0] = L.sx;
+        dst[1] = L.sy;
+        dst[2] = L.sz;
+        have_unit = false;
+      }
+    }
+  }
+  if constexpr (MODE == 1) {
+    atomicAdd(A.counts + 0, n_samples);
+    atomicAdd(A.counts + 1, n_segments);
+    atomicAdd(A.counts + 2, n_visits);
+    atomicAdd(A.counts + 3, n_tests);
+  }
+}
+
+size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * kWorldBlock * sizeof(uint32_t); }
+
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
+  if (mode == 1)
+    hipLaunchKernelGGL(world_kernel<1>, dim3(grid), dim3(kWorldBlock), lds, s, a);
+  else
+    hipLaunchKernelGGL(world_kernel<0>, dim3(grid), dim3(kWorldBlock), lds, s, a);
+  return hipGetLastError();
+}
+
+int world_blocks_per_cu(size_t lds) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0>, kWorldBlock, lds) != hipSuccess) nb = 0;
+  return nb > 0 ? nb : 1;
+}
+
+}  // namespace rtwk

@@ -1,0 +1,528 @@
+// rtw_world_capi.hip — C ABI of the general-world path (include/rtw_hip.h
+// "general worlds"): validation of an rtw_world_desc, packing into the
+// device records of rtw_internal.hpp, the BVH build, the render launches.
+// Replaces the render loop of main.zig:378-402 for scenes 2-6 (and 1, 7).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rtw_hip.h"
+#include "rtw_internal.hpp"
+
+// rtw_capi.hip helpers shared by both paths (same library).
+int rtw_fail(int status, const char* fmt, ...);
+int rtw_validate_params(const rtw_params* p);
+size_t rtw_ws_total(const rtw_params* p);
+int rtw_device_cus(int dev);
+void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, const rtw_params* p, unsigned char* ws);
+int rtw_launch_finalize(const rtw_params* p, unsigned char* ws, uint8_t* d_rgb, float* d_mean, hipStream_t s);
+size_t rtw_ws_stats_off(const rtw_params* p);
+size_t rtw_ws_counter_off(const rtw_params* p);
+int rtw_timer_mark(rtw_timer t, hipStream_t s, bool start);
+
+namespace {
+
+struct Box {
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], b.lo[k]), hi[k] = std::max(hi[k], b.hi[k]);
+  }
+  void grow(const double p[3]) {
+    for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], p[k]), hi[k] = std::max(hi[k], p[k]);
+  }
+  double area() const {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return dx < 0 ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+// World-space bounding box of a primitive: the reference's boudingBox
+// (hittable.zig:133-143 sphere, :203-217 moving sphere over the camera
+// shutter [0, 1], :304-317 / :359-372 / :414-427 rects padded by 1e-4)
+// through its Translate / RotateY chain (:493-501, :514-556).
+Box prim_box(const rtw_prim& p, const rtw_xform* xf) {
+  Box b;
+  if (p.kind <= RTW_PRIM_MOVING_SPHERE) {
+    const double r = std::fabs(p.a[6]);
+    for (int s = 0; s < (p.kind == RTW_PRIM_MOVING_SPHERE ? 2 : 1); ++s) {
+      double c[3];
+      for (int k = 0; k < 3; ++k) {
+        c[k] = p.kind == RTW_PRIM_MOVING_SPHERE ? p.a[k] + (p.a[3 + k] - p.a[k]) * (((double)s - p.a[7]) / (p.a[8] - p.a[7]))
+                                                : p.a[k];
+      }
+      Box cb;
+      for (int k = 0; k < 3; ++k) cb.lo[k] = c[k] - r, cb.hi[k] = c[k] + r;
+      b.grow(cb);
+    }
+  } else {
+    const int ax_k = p.kind == RTW_PRIM_XY_RECT ? 2 : (p.kind == RTW_PRIM_XZ_RECT ? 1 : 0);
+    const int ax_a = p.kind == RTW_PRIM_YZ_RECT ? 1 : 0, ax_b = p.kind == RTW_PRIM_XY_RECT ? 1 : 2;
+    b.lo[ax_a] = p.a[0], b.hi[ax_a] = p.a[1];
+    b.lo[ax_b] = p.a[2], b.hi[ax_b] = p.a[3];
+    b.lo[ax_k] = p.a[4] - 0.0001, b.hi[ax_k] = p.a[4] + 0.0001;
+  }
+  if (xf) {
+    for (int i = (int)xf->n - 1; i >= 0; --i) {
+      if (xf->op[i] == RTW_XF_TRANSLATE) {
+        for (int k = 0; k < 3; ++k) b.lo[k] += xf->v[i][k], b.hi[k] += xf->v[i][k];
+      } else {
+        const double sn = xf->v[i][0], cs = xf->v[i][1];
+        Box nb;
+        for (int c = 0; c < 8; ++c) {
+          const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1],
+                       z = (c & 4) ? b.hi[2] : b.lo[2];
+          const double q[3] = {cs * x + sn * z, y, -sn * x + cs * z};
+          nb.grow(q);
+        }
+        b = nb;
+      }
+    }
+  }
+  return b;
+}
+
+struct Bvh {
+  std::vector<double> nodes;  // kWorldRec per node
+  std::vector<uint32_t> order;  // stored position -> original prim index
+  uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
+};
+
+class Builder {
+ public:
+  Builder(const std::vector<Box>& boxes, Bvh& out) : boxes_(boxes), out_(out) {
+    idx_.resize(boxes.size());
+    for (size_t i = 0; i < idx_.size(); ++i) idx_[i] = (uint32_t)i;
+    for (const Box& b : boxes) {
+      double m[3];
+      for (int k = 0; k < 3; ++k) m[k] = 0.5 * (b.lo[k] + b.hi[k]);
+      cent_.push_back({m[0], m[1], m[2]});
+    }
+  }
+  void run() {
+    const uint32_t root = alloc();
+    node(root, 0, (uint32_t)idx_.size(), 0);
+    out_.order = idx_;
+  }
+
+ private:
+  const std::vector<Box>& boxes_;
+  Bvh& out_;
+  std::vector<uint32_t> idx_;
+  std::vector<std::array<double, 3>> cent_;
+
+  uint32_t alloc() {
+    out_.nodes.resize(out_.nodes.size() + rtwk::kWorldRec, 0.0);
+    return out_.n_nodes++;
+  }
+  Box range_box(uint32_t b, uint32_t e) const {
+    Box r;
+    for (uint32_t i = b; i < e; ++i) r.grow(boxes_[idx_[i]]);
+    return r;
+  }
+  uint32_t leaf(uint32_t b, uint32_t e) {
+    out_.n_leaves++;
+    out_.max_leaf = std::max(out_.max_leaf, e - b);
+    return rtwk::kLeafBit | ((e - b) << 23) | b;
+  }
+  // Binned SAH split of [b, e); falls back to the median of the widest axis.
+  uint32_t split(uint32_t b, uint32_t e, bool sah) {
+    Box cb;
+    for (uint32_t i = b; i < e; ++i) cb.grow(cent_[idx_[i]].data());
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    if (sah && cb.hi[axis] > cb.lo[axis]) {
+      constexpr int kBins = 16;
+      double best = INFINITY;
+      int best_axis = -1, best_bin = -1;
+      for (int k = 0; k < 3; ++k) {
+        const double ext = cb.hi[k] - cb.lo[k];
+        if (!(ext > 0)) continue;
+        Box bb[kBins];
+        uint32_t cnt[kBins] = {0};
+        for (uint32_t i = b; i < e; ++i) {
+          int t = (int)((cent_[idx_[i]][k] - cb.lo[k]) / ext * kBins);
+          t = std::min(std::max(t, 0), kBins - 1);
+          bb[t].grow(boxes_[idx_[i]]);
+          cnt[t]++;
+        }
+        Box left[kBins];
+        uint32_t lc[kBins];
+        Box acc;
+        uint32_t ac = 0;
+        for (int t = 0; t < kBins; ++t) acc.grow(bb[t]), ac += cnt[t], left[t] = acc, lc[t] = ac;
+        acc = Box();
+        ac = 0;
+        for (int t = kBins - 1; t > 0; --t) {
+          acc.grow(bb[t]);
+          ac += cnt[t];
+          const double cost = left[t - 1].area() * lc[t - 1] + acc.area() * ac;
+          if (lc[t - 1] > 0 && ac > 0 && cost < best) best = cost, best_axis = k, best_bin = t;
+        }
+      }
+      if (best_axis >= 0) {
+        const double ext = cb.hi[best_axis] - cb.lo[best_axis];
+        auto mid = std::partition(idx_.begin() + b, idx_.begin() + e, [&](uint32_t i) {
+          int t = (int)((cent_[i][best_axis] - cb.lo[best_axis]) / ext * kBins);
+          return std::min(std::max(t, 0), kBins - 1) < best_bin;
+        });
+        const uint32_t m = (uint32_t)(mid - idx_.begin());
+        if (m > b && m < e) return m;
+      }
+    }
+    const uint32_t m = b + (e - b) / 2;
+    std::nth_element(idx_.begin() + b, idx_.begin() + m, idx_.begin() + e,
+                     [&](uint32_t x, uint32_t y) { return cent_[x][axis] < cent_[y][axis]; });
+    return m;
+  }
+  uint32_t child(uint32_t b, uint32_t e, uint32_t depth) {
+    // Leaves: few primitives, or the depth cap of the per-lane LDS stack
+    // (node() switches to median splits while they still fit the cap).
+    if (e - b <= rtwk::kMaxLeafPrims || (depth >= rtwk::kBvhStack - 1 && e - b <= 255)) return leaf(b, e);
+    const uint32_t n = alloc();
+    node(n, b, e, depth);
+    return n;
+  }
+  void node(uint32_t n, uint32_t b, uint32_t e, uint32_t depth) {
+    out_.max_depth = std::max(out_.max_depth, depth + 1);
+    uint32_t m;
+    if (e - b <= rtwk::kMaxLeafPrims) {  // root of a tiny world: one leaf + an empty one
+      m = e;
+    } else {
+      // SAH while the median-split depth of the rest still fits the stack.
+      uint32_t need = 0;
+      for (uint32_t c = e - b; c > rtwk::kMaxLeafPrims; c = (c + 1) / 2) ++need;
+      m = split(b, e, depth + need + 2 < rtwk::kBvhStack);
+    }
+    const uint32_t c0 = m == e ? leaf(b, e) : child(b, m, depth + 1);
+    const uint32_t c1 = m == e ? (rtwk::kLeafBit | e) : child(m, e, depth + 1);
+    const Box b0 = range_box(b, m), b1 = range_box(m, e);
+    double* nd = out_.nodes.data() + (size_t)rtwk::kWorldRec * n;
+    for (int k = 0; k < 3; ++k) {
+      nd[k] = b0.lo[k], nd[3 + k] = b0.hi[k];
+      nd[6 + k] = b1.lo[k], nd[9 + k] = b1.hi[k];
+    }
+    uint32_t refs[2] = {c0, c1};
+    std::memcpy(nd + 12, refs, sizeof(refs));
+  }
+};
+
+}  // namespace
+
+struct rtw_world_s {
+  int device = 0;
+  void* buf = nullptr;
+  rtwk::WorldView view{};
+  Box bounds;
+  bool has_moving = false;
+  uint32_t info[4] = {0, 0, 0, 0};
+};
+
+extern "C" {
+
+int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
+  if (!out || !d) return rtw_fail(RTW_EINVAL, "rtw_world_create: desc/out is NULL");
+  *out = nullptr;
+  if ((d->n_prims && !d->prims) || (d->n_xforms && !d->xforms) || (d->n_textures && !d->textures) ||
+      (d->n_mats && !d->mats) || (d->n_perlins && !d->perlins) || (d->n_images && !d->images))
+    return rtw_fail(RTW_EINVAL, "rtw_world_create: NULL array with a non-zero count");
+  if (d->n_prims >= (1u << 23)) return rtw_fail(RTW_UNSUPPORTED, "%u primitives exceed 2^23", d->n_prims);
+  for (uint32_t i = 0; i < d->n_xforms; ++i) {
+    if (d->xforms[i].n > RTW_MAX_XFORM_OPS) return rtw_fail(RTW_EINVAL, "xform %u: %u ops", i, d->xforms[i].n);
+    for (uint32_t k = 0; k < d->xforms[i].n; ++k)
+      if (d->xforms[i].op[k] > RTW_XF_ROTATE_Y) return rtw_fail(RTW_EINVAL, "xform %u: op %u", i, d->xforms[i].op[k]);
+  }
+  for (uint32_t i = 0; i < d->n_images; ++i)
+    if (!d->images[i].rgba || !d->images[i].width || !d->images[i].height)
+      return rtw_fail(RTW_EINVAL, "image %u is empty", i);
+  for (uint32_t i = 0; i < d->n_textures; ++i) {
+    const rtw_texture& t = d->textures[i];
+    if (t.kind > RTW_TEX_IMAGE) return rtw_fail(RTW_EINVAL, "texture %u: kind %u", i, t.kind);
+    if (t.kind == RTW_TEX_NOISE && t.perlin >= d->n_perlins) return rtw_fail(RTW_EINVAL, "texture %u: perlin", i);
+    if (t.kind == RTW_TEX_IMAGE && t.image >= d->n_images) return rtw_fail(RTW_EINVAL, "texture %u: image", i);
+  }
+  for (uint32_t i = 0; i < d->n_mats; ++i) {
+    const rtw_wmaterial& m = d->mats[i];
+    if (m.kind > RTW_WMAT_LIGHT) return rtw_fail(RTW_EINVAL, "material %u: kind %u", i, m.kind);
+    if ((m.kind == RTW_WMAT_LAMBERT || m.kind == RTW_WMAT_LIGHT) && m.tex >= d->n_textures)
+      return rtw_fail(RTW_EINVAL, "material %u: texture %u >= %u", i, m.tex, d->n_textures);
+  }
+  rtw_world_s* w = new rtw_world_s;
+  std::vector<Box> boxes(d->n_prims);
+  for (uint32_t i = 0; i < d->n_prims; ++i) {
+    const rtw_prim& p = d->prims[i];
+    if (p.kind > RTW_PRIM_YZ_RECT || p.mat >= d->n_mats || p.xform >= (int32_t)d->n_xforms || p.xform < -1) {
+      delete w;
+      return rtw_fail(RTW_EINVAL, "prim %u: kind %u / material %u / xform %d out of range", i, p.kind, p.mat, p.xform);
+    }
+    boxes[i] = prim_box(p, p.xform >= 0 ? &d->xforms[p.xform] : nullptr);
+    w->bounds.grow(boxes[i]);
+    w->has_moving |= p.kind == RTW_PRIM_MOVING_SPHERE;
+  }
+  Bvh bvh;
+  const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > 0;
+  if (use_bvh) {
+    Builder(boxes, bvh).run();
+  } else {
+    for (uint32_t i = 0; i < d->n_prims; ++i) bvh.order.push_back(i);
+  }
+  // Device records, in stored (leaf) order; `order_dev` maps list index -> stored position.
+  const uint32_t n = d->n_prims;
+  std::vector<double> prim((size_t)rtwk::kWorldRec * std::max(n, 1u), 0.0);
+  std::vector<uint32_t> list_to_pos(n);
+  for (uint32_t pos = 0; pos < n; ++pos) {
+    const uint32_t li = bvh.order[pos];
+    list_to_pos[li] = pos;
+    const rtw_prim& p = d->prims[li];
+    double* r = prim.data() + (size_t)rtwk::kWorldRec * pos;
+    if (p.kind <= RTW_PRIM_MOVING_SPHERE) {
+      for (int k = 0; k < 3; ++k) r[k] = p.a[k];
+      if (p.kind == RTW_PRIM_MOVING_SPHERE) {
+        for (int k = 0; k < 3; ++k) r[3 + k] = p.a[3 + k] - p.a[k];  // center1.sub(center0)
+        r[7] = p.a[7];
+        r[8] = p.a[8] - p.a[7];  // time1 - time0
+      }
+      r[6] = p.a[6];
+      r[9] = p.a[6] * p.a[6];  // sphere.radius * sphere.radius
+    } else {
+      for (int k = 0; k < 5; ++k) r[k] = p.a[k];
+      r[5] = p.a[1] - p.a[0];
+      r[6] = p.a[3] - p.a[2];
+    }
+    const uint32_t meta[4] = {p.kind | ((uint32_t)(p.xform + 1) << 8), p.mat, li, 0u};
+    std::memcpy(r + 14, meta, sizeof(meta));
+  }
+  std::vector<double> xf((size_t)rtwk::kWorldRec * std::max(d->n_xforms, 1u), 0.0);
+  for (uint32_t i = 0; i < d->n_xforms; ++i) {
+    double* r = xf.data() + (size_t)rtwk::kWorldRec * i;
+    uint32_t h = d->xforms[i].n;
+    for (uint32_t k = 0; k < d->xforms[i].n; ++k) {
+      h |= d->xforms[i].op[k] << (8 + 4 * k);
+      for (int c = 0; c < 3; ++c) r[4 + 3 * k + c] = d->xforms[i].v[k][c];
+    }
+    std::memcpy(r, &h, 4);
+  }
+  std::vector<double> tex((size_t)rtwk::kWorldRec * std::max(d->n_textures, 1u), 0.0);
+  for (uint32_t i = 0; i < d->n_textures; ++i) {
+    const rtw_texture& t = d->textures[i];
+    double* r = tex.data() + (size_t)rtwk::kWorldRec * i;
+    const uint32_t h[4] = {t.kind, t.perlin, t.image, 0u};
+    std::memcpy(r, h, sizeof(h));
+    for (int c = 0; c < 3; ++c) r[2 + c] = t.color[c], r[5 + c] = t.odd[c], r[8 + c] = t.even[c];
+    r[11] = t.scale;
+  }
+  std::vector<double> mat((size_t)8 * std::max(d->n_mats, 1u), 0.0);
+  for (uint32_t i = 0; i < d->n_mats; ++i) {
+    const rtw_wmaterial& m = d->mats[i];
+    double* r = mat.data() + (size_t)8 * i;
+    const uint32_t h[2] = {m.kind, m.tex};
+    std::memcpy(r, h, sizeof(h));
+    for (int c = 0; c < 3; ++c) r[1 + c] = m.albedo[c];
+    r[4] = m.fuzz, r[5] = m.ir;
+  }
+  constexpr size_t kPerlinDoubles = 256 * 3 + 384;
+  std::vector<double> perl(kPerlinDoubles * std::max(d->n_perlins, 1u), 0.0);
+  for (uint32_t i = 0; i < d->n_perlins; ++i) {
+    double* r = perl.data() + kPerlinDoubles * i;
+    for (int j = 0; j < 256; ++j)
+      for (int c = 0; c < 3; ++c) r[3 * j + c] = d->perlins[i].ranvec[j][c];
+    std::memcpy(r + 256 * 3, d->perlins[i].perm, sizeof(d->perlins[i].perm));
+  }
+  std::vector<uint32_t> img(4 * std::max(d->n_images, 1u), 0u);
+  size_t pix_bytes = 0;
+  for (uint32_t i = 0; i < d->n_images; ++i) {
+    img[4 * i] = d->images[i].width, img[4 * i + 1] = d->images[i].height;
+    img[4 * i + 2] = (uint32_t)pix_bytes, img[4 * i + 3] = (uint32_t)(pix_bytes >> 32);
+    pix_bytes += (size_t)d->images[i].width * d->images[i].height * 4;
+  }
+  // One allocation: prim | xform | tex | mat | perlin | image | pixels | nodes + order
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t o_prim = 0, o_xf = o_prim + al(prim.size() * 8), o_tex = o_xf + al(xf.size() * 8);
+  const size_t o_mat = o_tex + al(tex.size() * 8), o_perl = o_mat + al(mat.size() * 8);
+  const size_t o_img = o_perl + al(perl.size() * 8), o_pix = o_img + al(img.size() * 4);
+  const size_t o_node = o_pix + al(std::max(pix_bytes, (size_t)4));
+  const size_t total = o_node + al(bvh.nodes.size() * 8 + (size_t)std::max(n, 1u) * 4);
+  std::vector<unsigned char> host(total, 0);
+  std::memcpy(host.data() + o_prim, prim.data(), prim.size() * 8);
+  std::memcpy(host.data() + o_xf, xf.data(), xf.size() * 8);
+  std::memcpy(host.data() + o_tex, tex.data(), tex.size() * 8);
+  std::memcpy(host.data() + o_mat, mat.data(), mat.size() * 8);
+  std::memcpy(host.data() + o_perl, perl.data(), perl.size() * 8);
+  std::memcpy(host.data() + o_img, img.data(), img.size() * 4);
+  for (uint32_t i = 0; i < d->n_images; ++i)
+    std::memcpy(host.data() + o_pix + ((size_t)img[4 * i + 2] | ((size_t)img[4 * i + 3] << 32)), d->images[i].rgba,
+                (size_t)d->images[i].width * d->images[i].height * 4);
+  if (!bvh.nodes.empty()) std::memcpy(host.data() + o_node, bvh.nodes.data(), bvh.nodes.size() * 8);
+  if (n) std::memcpy(host.data() + o_node + bvh.nodes.size() * 8, list_to_pos.data(), (size_t)n * 4);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    delete w;
+    return rtw_fail(RTW_ENODEV, "no HIP device");
+  }
+  if (hipMalloc(&w->buf, total) != hipSuccess) {
+    delete w;
+    return rtw_fail(RTW_ENOMEM, "rtw_world_create: hipMalloc(%zu)", total);
+  }
+  if (hipMemcpy(w->buf, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(w->buf);
+    delete w;
+    return rtw_fail(RTW_EHIP, "rtw_world_create: hipMemcpy failed");
+  }
+  auto* base = static_cast<unsigned char*>(w->buf);
+  w->device = dev;
+  w->view.prim = reinterpret_cast<const double*>(base + o_prim);
+  w->view.xform = reinterpret_cast<const double*>(base + o_xf);
+  w->view.tex = reinterpret_cast<const double*>(base + o_tex);
+  w->view.mat = reinterpret_cast<const double*>(base + o_mat);
+  w->view.perlin = reinterpret_cast<const double*>(base + o_perl);
+  w->view.image = reinterpret_cast<const uint32_t*>(base + o_img);
+  w->view.pixels = base + o_pix;
+  w->view.node = reinterpret_cast<const double*>(base + o_node);
+  w->view.n_prims = n;
+  w->view.n_nodes = bvh.n_nodes;
+  w->view.n_perlins = d->n_perlins;
+  w->info[0] = bvh.n_nodes, w->info[1] = bvh.n_leaves, w->info[2] = bvh.max_depth, w->info[3] = bvh.max_leaf;
+  *out = w;
+  return RTW_OK;
+}
+
+int rtw_world_destroy(rtw_world w) {
+  if (!w) return RTW_OK;
+  if (w->buf) (void)hipFree(w->buf);
+  delete w;
+  return RTW_OK;
+}
+
+int rtw_world_bvh_info(rtw_world w, uint32_t info_out[4]) {
+  if (!w || !info_out) return rtw_fail(RTW_EINVAL, "world/info is NULL");
+  std::memcpy(info_out, w->info, sizeof(w->info));
+  return RTW_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Widening of every BVH box test.  A computed sphere root deviates from the
+// exact intersection by at most ~sqrt(u * (hb^2 + |a c|)) / a (u = 2^-53; the
+// sqrt of a discriminant with absolute error u*(hb^2 + |ac|)), i.e. in space
+// by <= sqrt(u) * sqrt(2 |o - c|^2 + r^2) <= 2.2e-8 * L, where L bounds
+// |o - c| + r over every ray origin o (camera or a surface point) and
+// primitive.  Rect roots and the slab arithmetic are accurate to a few u * L.
+// margin = 1e-7 * L with L = 2 * (max |coordinate| of the scene box and the
+// camera) + 1 covers both with a 4x safety factor, so a box that holds a
+// primitive the linear list would accept is never pruned.
+double bvh_margin(const rtw_world_s* w, const rtw_camera* cam) {
+  double m = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (std::isfinite(w->bounds.lo[k])) m = std::max(m, std::fabs(w->bounds.lo[k]));
+    if (std::isfinite(w->bounds.hi[k])) m = std::max(m, std::fabs(w->bounds.hi[k]));
+    m = std::max(m, std::fabs(cam->origin[k]) + cam->lens_radius * 2);
+  }
+  return 1e-7 * (2.0 * m + 1.0);
+}
+
+int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
+                 uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode) {
+  if (!w || !cam) return rtw_fail(RTW_EINVAL, "world/camera is NULL");
+  const int v = rtw_validate_params(p);
+  if (v != RTW_OK) return v;
+  if (p->precision != RTW_PRECISION_F64 || p->engine != RTW_ENGINE_MEGAKERNEL)
+    return rtw_fail(RTW_UNSUPPORTED, "world renders run in f64 on the megakernel engine");
+  if (w->has_moving && w->view.n_nodes && (cam->time0 < 0.0 || cam->time1 > 1.0))
+    return rtw_fail(RTW_UNSUPPORTED, "BVH boxes of moving spheres cover shutter times [0, 1] only");
+  const size_t need = rtw_ws_total(p);
+  if (!ws || ws_bytes < need) return rtw_fail(RTW_EINVAL, "workspace %zu bytes < required %zu", ws_bytes, need);
+  if ((reinterpret_cast<uintptr_t>(ws) & 255) != 0) return rtw_fail(RTW_EINVAL, "workspace not 256-B aligned");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return rtw_fail(RTW_ENODEV, "no HIP device");
+  if (dev != w->device) return rtw_fail(RTW_EINVAL, "world lives on device %d, current is %d", w->device, dev);
+  auto* wsb = static_cast<unsigned char*>(ws);
+  if (hipMemsetAsync(wsb + rtw_ws_counter_off(p), 0, 512, stream) != hipSuccess)
+    return rtw_fail(RTW_EHIP, "workspace reset failed");
+  rtwk::WorldArgs a;
+  std::memset(&a, 0, sizeof(a));
+  rtw_fill_trace_args(a.t, cam, p, wsb);
+  a.w = w->view;
+  a.margin = bvh_margin(w, cam);
+  a.counts = reinterpret_cast<unsigned long long*>(wsb + rtw_ws_stats_off(p));
+  const size_t lds = rtwk::world_lds_bytes(w->view.n_perlins);
+  static int bpc_cache = 0;
+  if (bpc_cache == 0) bpc_cache = rtwk::world_blocks_per_cu(lds);
+  const uint32_t want = (a.t.total_units + 255) / 256;
+  const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc_cache), want));
+  if (timer && rtw_timer_mark(timer, stream, true) != RTW_OK) return RTW_EHIP;
+  hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode);
+  if (e != hipSuccess) return rtw_fail(RTW_EHIP, "world kernel launch: %s", hipGetErrorString(e));
+  if (timer && rtw_timer_mark(timer, stream, false) != RTW_OK) return RTW_EHIP;
+  if (d_rgb) return rtw_launch_finalize(p, wsb, d_rgb, d_mean, stream);
+  return RTW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
+                            uint8_t* d_rgb, float* d_mean, void* stream, rtw_timer timer) {
+  if (!d_rgb) return rtw_fail(RTW_EINVAL, "d_rgb is NULL");
+  return world_launch(w, cam, p, ws, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, 0);
+}
+
+int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
+                            uint64_t counts_out[4]) {
+  if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
+  const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1);
+  if (st != RTW_OK) return st;
+  if (hipDeviceSynchronize() != hipSuccess) return rtw_fail(RTW_EHIP, "world counts pass failed");
+  unsigned long long c[4];
+  if (hipMemcpy(c, static_cast<unsigned char*>(ws) + rtw_ws_stats_off(p), sizeof(c), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return rtw_fail(RTW_EHIP, "counts copy failed");
+  for (int i = 0; i < 4; ++i) counts_out[i] = c[i];
+  return RTW_OK;
+}
+
+int rtw_world_render(const rtw_camera* cam, const rtw_world_desc* desc, const rtw_params* p, uint8_t* rgb_out,
+                     float* mean_out) {
+  if (!cam || !desc || !rgb_out) return rtw_fail(RTW_EINVAL, "camera/desc/rgb_out is NULL");
+  const int v = rtw_validate_params(p);
+  if (v != RTW_OK) return v;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return rtw_fail(RTW_ENODEV, "no HIP device visible");
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return rtw_fail(RTW_EHIP, "hipGetDevice failed");
+  const int dev = p->device < 0 ? prev : p->device;
+  if (dev >= ndev) return rtw_fail(RTW_EINVAL, "device %d >= device count %d", dev, ndev);
+  if (hipSetDevice(dev) != hipSuccess) return rtw_fail(RTW_EHIP, "hipSetDevice failed");
+  rtw_world w = nullptr;
+  int st = rtw_world_create(desc, 0, &w);
+  const size_t wsb = rtw_ws_total(p), pix = (size_t)p->row_count * p->width * 3;
+  void *ws = nullptr, *d_rgb = nullptr, *d_mean = nullptr;
+  if (st == RTW_OK && (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&d_rgb, pix) != hipSuccess ||
+                       (mean_out && hipMalloc(&d_mean, pix * sizeof(float)) != hipSuccess)))
+    st = rtw_fail(RTW_ENOMEM, "rtw_world_render: device allocation failed");
+  if (st == RTW_OK)
+    st = world_launch(w, cam, p, ws, wsb, static_cast<uint8_t*>(d_rgb), static_cast<float*>(d_mean), nullptr,
+                      nullptr, 0);
+  if (st == RTW_OK && hipDeviceSynchronize() != hipSuccess) st = rtw_fail(RTW_EHIP, "world render failed on the device");
+  if (st == RTW_OK && hipMemcpy(rgb_out, d_rgb, pix, hipMemcpyDeviceToHost) != hipSuccess)
+    st = rtw_fail(RTW_EHIP, "copy of rgb_out failed");
+  if (st == RTW_OK && mean_out && hipMemcpy(mean_out, d_mean, pix * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    st = rtw_fail(RTW_EHIP, "copy of mean_out failed");
+  if (ws) (void)hipFree(ws);
+  if (d_rgb) (void)hipFree(d_rgb);
+  if (d_mean) (void)hipFree(d_mean);
+  rtw_world_destroy(w);
+  (void)hipSetDevice(prev);
+  return st;
+}
+
+}  // extern "C"

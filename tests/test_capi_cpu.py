@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol(rtw):
 
 
 def test_abi_version(rtw):
-    assert rtw.abi_version() == 2
+    assert rtw.abi_version() == 3
 
 
 def test_struct_layouts_match_header(rtw):
