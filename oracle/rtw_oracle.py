@@ -418,3 +418,72 @@ class OracleWorld:
 def libm(name: str):
     """The Tier-B transcendental (ro_libm.h) as a Python callable."""
     return getattr(_world_lib(), "rw_" + name)
+
+
+class TableWorld(OracleWorld):
+    """An oracle world built from plain tables (e.g. a product rtw_world_desc
+    read back through ctypes) instead of rw_scene: prims / xforms / textures /
+    materials / perlins as lists of the WPrim/WXform/... field dicts, images
+    as (H, W, 4) uint8 arrays."""
+
+    def __init__(self, prims, xforms=(), textures=(), materials=(), perlins=(), images=(), background=(0, 0, 0)):
+        _world_lib()
+        self.rng = ZigRandom(0)
+        self.ptr = None
+        self.scene_id = 0
+        self._keep = []
+
+        def arr(typ, items, fill):
+            a = (typ * max(1, len(items)))()
+            for i, it in enumerate(items):
+                fill(a[i], it)
+            self._keep.append(a)
+            return C.cast(a, C.POINTER(typ))
+
+        def f_prim(d, p):
+            d.kind, d.mat, d.xform = p["kind"], p["mat"], p["xform"]
+            d.a[:] = list(p["a"]) + [0.0] * (9 - len(p["a"]))
+
+        def f_xf(d, x):
+            d.n = x["n"]
+            for k in range(x["n"]):
+                d.op[k] = x["op"][k]
+                d.v[k][:] = x["v"][k]
+
+        def f_tex(d, t):
+            d.kind, d.perlin, d.image = t["kind"], t.get("perlin", 0), t.get("image", 0)
+            d.color[:], d.odd[:], d.even[:] = t.get("color", (0, 0, 0)), t.get("odd", (0, 0, 0)), t.get("even", (0, 0, 0))
+            d.scale = t.get("scale", 0.0)
+
+        def f_mat(d, m):
+            d.kind, d.tex = m["kind"], m.get("tex", 0)
+            d.albedo[:] = m.get("albedo", (0, 0, 0))
+            d.fuzz, d.ir = m.get("fuzz", 0.0), m.get("ir", 0.0)
+
+        def f_perlin(d, p):
+            for k in range(256):
+                d.ranvec[k][:] = p["ranvec"][k]
+            for a in range(3):
+                d.perm[a][:] = p["perm"][a]
+
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
+        self._keep.extend(imgs)
+
+        def f_img(d, im):
+            d.width, d.height, d.rgba = im.shape[1], im.shape[0], im.ctypes.data
+
+        w = World()
+        w.n_prims, w.n_xforms, w.n_textures = len(prims), len(xforms), len(textures)
+        w.n_mats, w.n_perlins, w.n_images = len(materials), len(perlins), len(imgs)
+        w.prims = arr(WPrim, prims, f_prim)
+        w.xforms = arr(WXform, xforms, f_xf)
+        w.textures = arr(WTexture, textures, f_tex)
+        w.mats = arr(WMaterial, materials, f_mat)
+        w.perlins = arr(WPerlin, perlins, f_perlin)
+        w.images = arr(WImage, imgs, f_img)
+        w.background[:] = background
+        self.w = w
+        self.ptr = C.pointer(w)
+
+    def close(self):
+        self.ptr = None
