@@ -20,8 +20,10 @@ Extra fields: roofline (dominant kernel = trace; HIP events on the render
 stream), cpu_baseline (oracle Tier A = the reference's algorithm, sequential
 RNG, one core, on a bounded sample of the same frame), f32_hybrid_variant,
 wavefront_variant (BASELINE configs[3]: the same frame on the wavefront
-engine, bit-identical image, with its HBM roofline).  --engine wavefront makes
-the wavefront engine the headline.
+engine, bit-identical image, with its HBM roofline), globe_10k_variant
+(configs[4]: globe + 10k spheres through the BVH world kernel) and
+cornell_variant (scene 6, the reference's default scene) at N = 1.
+--engine wavefront makes the wavefront engine the headline.
 """
 from __future__ import annotations
 
@@ -53,6 +55,7 @@ def parse():
                     help="headline engine (the other one is reported as a variant)")
     ap.add_argument("--wf-paths", type=int, default=0, help="wavefront in-flight paths (0 = library default)")
     ap.add_argument("--no-wavefront-variant", action="store_true")
+    ap.add_argument("--no-world-variants", action="store_true", help="skip the configs[4] globe and Cornell lines")
     ap.add_argument("--spp", type=int, default=SPP, help="spp per GPU (default 500 = configs[1])")
     ap.add_argument("--width", type=int, default=W_IMG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -94,6 +97,61 @@ def cpu_baseline(width, height, spp_sample):
     return {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
                       f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
+
+
+def world_variant(R, torch, scene, steps, warmup):
+    """A general-world scene on the world kernel (csrc/rtw_world.hip) at the
+    scene's own main.zig settings: scene 6 (Cornell box, the reference's
+    default scene, 600x600x200) or 7 (BASELINE configs[4]: globe + 10k
+    spheres, BVH, 1200x675x100; synthetic stand-in for the globe texture).
+    Timed with HIP events around the world kernel; a counts pass gives the
+    BVH statistics.  Record bytes = 128 B per node visit and per primitive
+    test (the traversal's data movement, served from L2/MALL)."""
+    from rtw_amd import world as Wd
+    earth = Wd.synthetic_world_map()
+    b = Wd.BuiltScene(scene, SEED, image=earth if scene in (4, 7) else None)
+    s = b.settings
+    cam = b.camera()
+    p = R.make_params(s.width, s.height, s.spp, DEPTH, SEED, background=b.background)
+    dw = Wd.DeviceWorld(b.desc)
+    need = R.workspace_bytes(p)
+    ws = torch.empty(need + 256, dtype=torch.uint8, device="cuda:0")
+    ptr = (ws.data_ptr() + 255) & ~255
+    rgb = torch.empty((s.height, s.width, 3), dtype=torch.uint8, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(max(1, warmup)):
+        dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st)
+    torch.cuda.synchronize()
+    timers = [R.Timer() for _ in range(steps)]
+    a = time.perf_counter()
+    for i in range(steps):
+        dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st, timers[i])
+    torch.cuda.synchronize()
+    e = time.perf_counter() - a
+    ms = sum(t.elapsed_ms() for t in timers) / steps
+    for t in timers:
+        t.close()
+    c = dw.counts(cam, p, ptr, need)
+    info = dw.bvh_info()
+    dw.close()
+    samples = s.width * s.height * s.spp
+    if info["nodes"] == 0:  # linear world: wave-uniform scalar record loads, no per-lane data movement
+        roof = {"bound": "issue/latency (wave-uniform scalar-loaded records; no BVH)", "achieved": None,
+                "unit": None, "peak": None, "frac": None}
+    else:
+        rec_bytes = 128 * (c["node_visits"] + c["prim_tests"])
+        gbs = rec_bytes / (ms * 1e-3) / 1e9
+        roof = {"bound": "latency (divergent per-lane node/primitive fetches; L2/MALL-resident tables)",
+                "achieved": round(gbs, 1), "unit": "GB/s of per-lane record fetches", "peak": PEAK_HBM_GBS,
+                "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    return {"value": round(samples * steps / e / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(e / steps * 1e3, 3),
+            "kernel_ms": round(ms, 3), "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
+                                                  "height": s.height, "spp": s.spp, "max_depth": DEPTH},
+            "bvh": info, "segments_per_sample": round(c["segments"] / samples, 3),
+            "node_visits_per_segment": round(c["node_visits"] / max(1, c["segments"]), 2),
+            "prim_tests_per_segment": round(c["prim_tests"] / max(1, c["segments"]), 2),
+            "roofline": roof,
+            "note": "world kernel, f64, bit-identical to oracle Tier B (tests/test_gpu_world.py)"}
 
 
 def wavefront_bytes(counts, precision, units):
@@ -289,6 +347,10 @@ def main():
     if not args.no_wavefront_variant and args.engine == "megakernel":
         extra["wavefront_variant"] = wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts,
                                                        samples_all, world, rank, dist, gather_image, torch)
+
+    if world == 1 and not args.no_world_variants:
+        extra["globe_10k_variant"] = world_variant(R, torch, 7, max(2, args.steps // 2), 1)
+        extra["cornell_variant"] = world_variant(R, torch, 6, max(2, args.steps // 2), 1)
 
     res = {
         "metric": "Msamples/sec (pixels x spp / s), RTIOW cover scene; trace-kernel roofline",

@@ -264,8 +264,9 @@ int rtw_built_scene_desc(rtw_built_scene b, rtw_world_desc *desc, rtw_scene_sett
                          uint64_t rng_state_after[4]);
 int rtw_built_scene_free(rtw_built_scene b);
 
-/* Upload a world to the CURRENT device: tables + a BVH (flags bit 0 =
- * RTW_WORLD_LINEAR: no BVH, test every primitive). */
+/* Upload a world to the CURRENT device: tables + a BVH over worlds of more
+ * than 32 primitives (flags bit 0 = RTW_WORLD_LINEAR: no BVH, every segment
+ * tests every primitive in a wave-uniform loop). */
 #define RTW_WORLD_LINEAR 1u
 typedef struct rtw_world_s *rtw_world;
 int rtw_world_create(const rtw_world_desc *desc, uint32_t flags, rtw_world *out);

@@ -187,8 +187,9 @@ struct WorldArgs {
   unsigned long long* counts;  // stats pass: {samples, segments, node visits, prim tests}
 };
 
-hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode);
-int world_blocks_per_cu(size_t lds);
+// occ: register-allocation target (workgroups per CU): 1 (none), 3 or 4.
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ);
+int world_blocks_per_cu(size_t lds, int occ);
 constexpr int kWorldBlock = 256;
 size_t world_lds_bytes(uint32_t n_perlins);
 

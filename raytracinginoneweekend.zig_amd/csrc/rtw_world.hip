@@ -218,23 +218,25 @@ __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v
       const uint32_t* perm = reinterpret_cast<const uint32_t*>(pr + 256 * 3);
       D accum = 0.0, weight = 1.0;
       V q = p;
+      // Rolled loops (one corner at a time): unrolled, the 56 corner
+      // evaluations would set the whole kernel's register budget.
+#pragma unroll 1
       for (int oct = 0; oct < 7; ++oct) {
         const D fx = floor(q.x), fy = floor(q.y), fz = floor(q.z);
         const D uu0 = q.x - fx, vv0 = q.y - fy, ww0 = q.z - fz;
         const D uu = uu0 * uu0 * (3 - 2 * uu0), vv = vv0 * vv0 * (3 - 2 * vv0), ww = ww0 * ww0 * (3 - 2 * ww0);
         const int i = (int)fx, j = (int)fy, k = (int)fz;
         D nz = 0.0;
-        for (int di = 0; di < 2; ++di)
-          for (int dj = 0; dj < 2; ++dj)
-            for (int dk = 0; dk < 2; ++dk) {
-              const uint32_t ix = (uint32_t)(i + di) & 255u, iy = (uint32_t)(j + dj) & 255u,
-                             iz = (uint32_t)(k + dk) & 255u;
-              const D* c = pr + 3 * (perm[ix] ^ perm[256 + iy] ^ perm[512 + iz]);
-              const D ti = (D)di, tj = (D)dj, tk = (D)dk;
-              const V wgt = mk(uu - ti, vv - tj, ww - tk);
-              nz += (ti * uu + (1.0 - ti) * (1.0 - uu)) * (tj * vv + (1.0 - tj) * (1.0 - vv)) *
-                    (tk * ww + (1.0 - tk) * (1.0 - ww)) * dot(ld3(c), wgt);
-            }
+#pragma unroll 1
+        for (int cr = 0; cr < 8; ++cr) {  // perlinInterp's i, j, k loops (perlin.zig:104-124), in order
+          const int di = cr >> 2, dj = (cr >> 1) & 1, dk = cr & 1;
+          const uint32_t ix = (uint32_t)(i + di) & 255u, iy = (uint32_t)(j + dj) & 255u, iz = (uint32_t)(k + dk) & 255u;
+          const D* c = pr + 3 * (perm[ix] ^ perm[256 + iy] ^ perm[512 + iz]);
+          const D ti = (D)di, tj = (D)dj, tk = (D)dk;
+          const V wgt = mk(uu - ti, vv - tj, ww - tk);
+          nz += (ti * uu + (1.0 - ti) * (1.0 - uu)) * (tj * vv + (1.0 - tj) * (1.0 - vv)) *
+                (tk * ww + (1.0 - tk) * (1.0 - ww)) * dot(ld3(c), wgt);
+        }
         accum += weight * nz;
         weight *= 0.5;
         q = mk(q.x * 2.0, q.y * 2.0, q.z * 2.0);
@@ -262,8 +264,10 @@ __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v
   }
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(kWorldBlock) world_kernel(WorldArgs A) {
+// OCC: minimum resident workgroups per CU asked of the register allocator
+// (1 = unconstrained; chosen by A/B on MI355X, rtw_world_capi.hip).
+template <int MODE, int OCC>
+__global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + threadIdx.x;
   const WorldView W = A.w;  // a local copy: no reference to the by-value argument escapes
@@ -486,18 +490,33 @@ __global__ void __launch_bounds__(kWorldBlock) world_kernel(WorldArgs A) {
 
 size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * kWorldBlock * sizeof(uint32_t); }
 
-hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
+template <int OCC>
+static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
   if (mode == 1)
-    hipLaunchKernelGGL(world_kernel<1>, dim3(grid), dim3(kWorldBlock), lds, s, a);
+    hipLaunchKernelGGL((world_kernel<1, OCC>), dim3(grid), dim3(kWorldBlock), lds, s, a);
   else
-    hipLaunchKernelGGL(world_kernel<0>, dim3(grid), dim3(kWorldBlock), lds, s, a);
+    hipLaunchKernelGGL((world_kernel<0, OCC>), dim3(grid), dim3(kWorldBlock), lds, s, a);
+}
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ) {
+  if (occ >= 4)
+    launch_occ<4>(a, grid, lds, s, mode);
+  else if (occ == 3)
+    launch_occ<3>(a, grid, lds, s, mode);
+  else
+    launch_occ<1>(a, grid, lds, s, mode);
   return hipGetLastError();
 }
 
-int world_blocks_per_cu(size_t lds) {
+int world_blocks_per_cu(size_t lds, int occ) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0>, kWorldBlock, lds) != hipSuccess) nb = 0;
-  return nb > 0 ? nb : 1;
+  hipError_t e;
+  if (occ >= 4)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 4>, kWorldBlock, lds);
+  else if (occ == 3)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 3>, kWorldBlock, lds);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 1>, kWorldBlock, lds);
+  return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 
 }  // namespace rtwk

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -267,7 +268,12 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     w->has_moving |= p.kind == RTW_PRIM_MOVING_SPHERE;
   }
   Bvh bvh;
-  const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > 0;
+  // Small worlds (<= kLinearMax primitives: the Cornell box, the Perlin and
+  // earth scenes) run the wave-uniform linear loop: every lane tests the same
+  // scalar-loaded record, which beat the divergent per-lane BVH walk on
+  // MI355X; RTW_WORLD_LINEAR forces it for any size.
+  constexpr uint32_t kLinearMax = 32;
+  const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
   } else {
@@ -410,6 +416,8 @@ int rtw_world_bvh_info(rtw_world w, uint32_t info_out[4]) {
 
 namespace {
 
+constexpr int kWorldOccDefault = 1;
+
 // Widening of every BVH box test.  A computed sphere root deviates from the
 // exact intersection by at most ~sqrt(u * (hb^2 + |a c|)) / a (u = 2^-53; the
 // sqrt of a discriminant with absolute error u*(hb^2 + |ac|)), i.e. in space
@@ -454,12 +462,18 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   a.margin = bvh_margin(w, cam);
   a.counts = reinterpret_cast<unsigned long long*>(wsb + rtw_ws_stats_off(p));
   const size_t lds = rtwk::world_lds_bytes(w->view.n_perlins);
-  static int bpc_cache = 0;
-  if (bpc_cache == 0) bpc_cache = rtwk::world_blocks_per_cu(lds);
+  // Register-allocation target (RTW_WORLD_OCC development knob; default from
+  // the A/B on MI355X).
+  const char* oc = getenv("RTW_WORLD_OCC");
+  const int occ = (oc && *oc) ? atoi(oc) : kWorldOccDefault;
+  static int bpc_cache[5] = {0, 0, 0, 0, 0};
+  const int oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
+  if (bpc_cache[oi] == 0) bpc_cache[oi] = rtwk::world_blocks_per_cu(lds, oi);
+  const int bpc = bpc_cache[oi];
   const uint32_t want = (a.t.total_units + 255) / 256;
-  const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc_cache), want));
+  const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
   if (timer && rtw_timer_mark(timer, stream, true) != RTW_OK) return RTW_EHIP;
-  hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode);
+  hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode, oi);
   if (e != hipSuccess) return rtw_fail(RTW_EHIP, "world kernel launch: %s", hipGetErrorString(e));
   if (timer && rtw_timer_mark(timer, stream, false) != RTW_OK) return RTW_EHIP;
   if (d_rgb) return rtw_launch_finalize(p, wsb, d_rgb, d_mean, stream);
