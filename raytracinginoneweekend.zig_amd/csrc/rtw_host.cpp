@@ -311,6 +311,7 @@ std::vector<uint8_t> render(const Camera& cam, const Hittable& world, const Rend
   p.chunk = s.chunk;
   p.precision = s.precision;
   p.device = -1;
+  p.engine = s.engine;
   const rtw_camera c = cam.to_c();
   std::vector<uint8_t> rgb((size_t)s.width * height * 3);
   const int st = rtw_render(&c, f.spheres.data(), (uint32_t)f.spheres.size(), f.materials.data(),

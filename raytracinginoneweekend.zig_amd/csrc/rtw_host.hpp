@@ -181,6 +181,7 @@ struct RenderSettings {
   Color background = rgb(0.70, 0.80, 1.00);
   uint32_t precision = RTW_PRECISION_F64;
   uint32_t chunk = 0;
+  uint32_t engine = RTW_ENGINE_MEGAKERNEL;  // or RTW_ENGINE_WAVEFRONT (same image)
 };
 uint32_t imageHeight(uint32_t width, double aspect_ratio);  // main.zig:306
 

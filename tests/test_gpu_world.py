@@ -211,3 +211,45 @@ def test_world_custom_every_feature(rtw, oracle, W, earth, bg):
     ref, _ = o.render_tier_b(oc, 128, 72, 8, chunk=3, bg=bg)
     assert_parity(g, ref, f"custom world bg {bg}")
     assert g.std() > 5  # not a blank frame
+
+
+def _write_png(path, rgba):
+    import struct
+    import zlib
+    h, w, _ = rgba.shape
+    raw = b"".join(b"\x00" + rgba[y].tobytes() for y in range(h))
+
+    def chunk(t, body):
+        return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body))
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)) +
+                chunk(b"IDAT", zlib.compress(raw)) + chunk(b"IEND", b""))
+
+
+def _read_ppm(path):
+    data = open(path, "rb").read()
+    parts = data.split(b"\n", 3)
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], np.uint8).reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("scene", [6, 4])
+def test_cli_renders_reference_scenes(rtw, oracle, W, earth, scene, tmp_path):
+    """bin/rtw_render (the reference's main() with the GPU loop): scene 6 is
+    the reference's default; scene 4 reads its earth texture from a PNG
+    through the CLI's own decoder.  Output equals oracle Tier B."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(W.__file__), "..", "bin", "rtw_render")
+    out = str(tmp_path / "out.ppm")
+    args = [exe, "--scene", str(scene), "--width", "64", "--spp", "4", "--out", out]
+    if scene == 4:
+        png = str(tmp_path / "earth.png")
+        _write_png(png, earth)
+        args += ["--image", png]
+    p = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    g = _read_ppm(out)
+    o = oracle.OracleWorld(scene, 42, image=earth if scene == 4 else None)
+    ref, _ = o.render_tier_b(o.camera(), g.shape[1], g.shape[0], 4)
+    assert_parity(g, ref, f"cli scene {scene}")
