@@ -159,13 +159,16 @@ hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* li
 //   material (8 doubles): {u32 kind, tex}, albedo, fuzz, ir at 1, 4, 5
 //   perlin : ranvec 256 x 3 f64, then perm 3 x 256 u32 (per perlin)
 //   image  : {width, height, byte offset} + one RGBA8 byte pool
-//   node   : BVH2 with both child boxes in the parent: lo0.xyz, hi0.xyz, lo1.xyz,
-//            hi1.xyz, {u32 ref0, ref1}; ref bit 31 = leaf {first (bits 0-22), count (23-30)}
+//   node   : 64 B, BVH2 with both child boxes in the parent: f32 lo0.xyz, hi0.xyz,
+//            lo1.xyz, hi1.xyz (each f64 box bound rounded OUTWARD to f32, so a box only
+//            grows), u32 ref0, ref1; ref bit 31 = leaf {first (bits 0-22), count (23-30)}
+//   order  : list index -> stored position (the NaN fallback's sequential loop)
 // Prims are stored in BVH leaf order; `orig` keeps the list index for the
 // reference's tie rule (later object wins).
-constexpr uint32_t kWorldRec = 16;
+constexpr uint32_t kWorldRec = 16;   // doubles per prim / xform / texture record
+constexpr uint32_t kNodeWords = 16;  // 32-bit words per BVH node
 constexpr uint32_t kLeafBit = 0x80000000u;
-constexpr uint32_t kBvhStack = 32;  // per-lane LDS stack entries (the builder caps the depth)
+constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder caps the depth)
 constexpr uint32_t kMaxLeafPrims = 4;
 
 struct WorldView {
@@ -176,7 +179,8 @@ struct WorldView {
   const double* perlin;
   const uint32_t* image;   // n_images x {width, height, offset_lo, offset_hi}
   const uint8_t* pixels;
-  const double* node;
+  const float* node;
+  const uint32_t* order;
   uint32_t n_prims, n_nodes, n_perlins, pad;
 };
 

@@ -6,10 +6,9 @@
 // Perlin noise, image), for every scene of main.zig and BASELINE.json
 // configs[4] (globe + 10k spheres).  f64, the reference's arithmetic.
 //
-// Closest hit: BVH2 traversal (both child boxes in the parent node) with a
-// per-lane stack in LDS (kBvhStack entries per lane, column-interleaved so
-// the 64 lanes of a wave hit 64 distinct banks), or a wave-uniform linear
-// loop for small worlds.  The reference's HittableList.hit picks the object of
+// Closest hit: wave-cooperative BVH2 traversal (both child boxes in the
+// parent node; one stack per wave in LDS; scalar-loaded nodes and
+// primitives), or a wave-uniform linear loop for small worlds.  The reference's HittableList.hit picks the object of
 // minimal effective root, ties to the later object — an order-independent
 // rule — so visiting primitives in BVH order returns the
 // same winner as long as no box that could hold a winner is pruned: every
@@ -35,13 +34,14 @@ using V = V3<D>;
 __device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
 
 // Translate / RotateY chains (hittable.zig:478-491, :561-600), op 0 outermost.
-__device__ __forceinline__ void to_object(const D* xf, V& o, V& d) {
-  const uint32_t h = *reinterpret_cast<const uint32_t*>(xf);
+template <typename P>
+__device__ __forceinline__ void to_object(P xf, V& o, V& d) {
+  const uint32_t h = (uint32_t)__builtin_bit_cast(uint64_t, (D)xf[0]);
   const uint32_t n = h & 0xFFu;
   for (uint32_t i = 0; i < n; ++i) {
-    const D* v = xf + 4 + 3 * i;
+    const auto v = xf + 4 + 3 * i;
     if (((h >> (8 + 4 * i)) & 0xFu) == 0u) {
-      o = sub(o, ld3(v));
+      o = sub(o, mk((D)v[0], (D)v[1], (D)v[2]));
     } else {
       const D sn = v[0], cs = v[1];
       const V o0 = o, d0 = d;
@@ -69,18 +69,36 @@ __device__ __forceinline__ void to_world(const D* xf, V& p, V& nrm) {
   }
 }
 
+// The fields of a primitive record the closest-hit test reads (doubles 0-9
+// and the meta words), loaded in one place so the linear loop can prefetch
+// the next record (scalar loads through the constant address space) while
+// the current one is tested.
+struct PrimRec {
+  D v[10];
+  uint32_t meta0, orig;
+};
+template <typename P>
+__device__ __forceinline__ PrimRec load_rec(P r) {
+  PrimRec q;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) q.v[i] = r[i];
+  // meta u32 {kind | xform+1 << 8, mat, orig, 0} occupies doubles 14-15
+  q.meta0 = (uint32_t)__builtin_bit_cast(uint64_t, (D)r[14]);
+  q.orig = (uint32_t)__builtin_bit_cast(uint64_t, (D)r[15]);
+  return q;
+}
+
 // The primitive's effective root for ray (o, d) in world space: Sphere.hit /
 // MovingSphere.hit root selection (hittable.zig:96-116, :166-187) or the rect
 // plane hit with its containment test (:278-286, :333-341, :388-396).
 // Returns false when the primitive cannot be hit at t >= tmin; t may be NaN.
-__device__ __forceinline__ bool prim_root(const WorldView& W, const D* r, V o, V d, D time, D tmin, D& t) {
-  const uint32_t* m = meta_of(r);
-  const uint32_t kind = m[0] & 0xFFu;
-  const int xf = (int)(m[0] >> 8) - 1;
-  if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+// root_obj: (o, d) already in the primitive's object space.
+__device__ __forceinline__ bool root_obj(const PrimRec& q, const V& o, const V& d, D time, D tmin, D& t) {
+  const D* r = q.v;
+  const uint32_t kind = q.meta0 & 0xFFu;
   if (kind <= 1u) {
-    V c = ld3(r);
-    if (kind == 1u) c = add(c, mul(ld3(r + 3), (time - r[7]) / r[8]));  // hittable.zig:219-221
+    V c = mk(r[0], r[1], r[2]);
+    if (kind == 1u) c = add(c, mul(mk(r[3], r[4], r[5]), (time - r[7]) / r[8]));  // hittable.zig:219-221
     const V oc = sub(o, c);
     const D a = norm2(d);
     const D hb = dot(oc, d);
@@ -108,6 +126,20 @@ __device__ __forceinline__ bool prim_root(const WorldView& W, const D* r, V o, V
   t = tt;
   return true;
 }
+__device__ __forceinline__ bool prim_root(const WorldView& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
+  const int xf = (int)(q.meta0 >> 8) - 1;
+  if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+  return root_obj(q, o, d, time, tmin, t);
+}
+
+// The adjacent f32 toward +inf / -inf (finite or infinite x; NaN kept).
+__device__ __forceinline__ float next_up(float x) {
+  if (!(x < __builtin_inff())) return x;
+  if (x == 0.0f) return __uint_as_float(1u);
+  const uint32_t b = __float_as_uint(x);
+  return __uint_as_float(x > 0.0f ? b + 1u : b - 1u);
+}
+__device__ __forceinline__ float next_down(float x) { return -next_up(-x); }
 
 struct WHit {
   int pos;     // stored position of the winner (-1: miss)
@@ -133,9 +165,8 @@ __device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* orde
   h.t = (D)__builtin_huge_val();
   for (uint32_t i = 0; i < W.n_prims; ++i) {
     const uint32_t k = order[i];
-    const D* r = W.prim + kWorldRec * k;
     D t;
-    if (!prim_root(W, r, o, d, time, tmin, t)) continue;
+    if (!prim_root(W, load_rec(W.prim + kWorldRec * k), o, d, time, tmin, t)) continue;
     if (h.t < t) continue;  // `t_max < root` rejects; NaN roots are accepted (as in the reference)
     h.t = t;
     h.pos = (int)k;
@@ -150,50 +181,92 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
   h.orig = -1;
   h.t = (D)__builtin_huge_val();
   h.nan = false;
-  if (W.n_nodes == 0) {  // linear: wave-uniform loop, scalar-loaded records
+  if (W.n_nodes == 0) {  // linear: wave-uniform loop, scalar-loaded records, one-ahead prefetch
+    const RTW_CONST D* pr = cptr(W.prim);
+    PrimRec cur = load_rec(pr);  // (a padding record follows the last primitive)
+    int xf_cur = -1;             // wave-uniform: the transform the cached object-space ray is for
+    V oo = o, od = d;
     for (uint32_t k = 0; k < W.n_prims; ++k) {
-      const D* r = W.prim + kWorldRec * k;
+      const PrimRec nxt = load_rec(pr + kWorldRec * (k + 1));
+      const int xf = (int)(cur.meta0 >> 8) - 1;
+      if (xf != xf_cur) {  // consecutive primitives share a chain (a Box's six rects)
+        xf_cur = xf;
+        oo = o, od = d;
+        if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
+      }
       D t;
       if (MODE == 1) ++nt;
-      if (prim_root(W, r, o, d, time, tmin, t)) accept(h, t, (int)k, (int)meta_of(r)[2], tmin);
+      if (root_obj(cur, oo, od, time, tmin, t)) accept(h, t, (int)k, (int)cur.orig, tmin);
+      cur = nxt;
     }
     return;
   }
+  // Wave-cooperative BVH traversal: the wave walks ONE stack (wave-uniform,
+  // in LDS) and descends into a child when ANY of its active lanes' rays
+  // hits the child's box; a leaf's primitives are tested by every active
+  // lane.  Node and primitive records are therefore wave-uniform (scalar
+  // loads, no per-lane memory divergence, no divergent control flow), and
+  // testing a primitive whose box a lane missed is harmless: acceptance is
+  // the exact rule of §5.1, the box test only prunes.
+  // Packed-f32 slab tests (two children per v_pk_fma_f32), conservative: the
+  // f32 node bounds are rounded outward and every box is widened by a margin
+  // that also covers the f32 rounding; the interval is
+  // compared with tmin rounded down and the closest root rounded up.
   const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
-  uint32_t sp = 0, node = 0;
+  const f2 ix = bc((float)inv.x), iy = bc((float)inv.y), iz = bc((float)inv.z);
+  const f2 ox = bc(-(float)o.x) * ix, oy = bc(-(float)o.y) * iy, oz = bc(-(float)o.z) * iz;
+  const float mf = (float)m;
+  const float tminf = next_down((float)tmin);
+  const RTW_CONST float* cn = cptr(W.node);
+  const RTW_CONST D* pr = cptr(W.prim);
+  uint32_t sp = 0, node = 0;  // wave-uniform
   auto leaf = [&](uint32_t ref) {
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & 0xFFu;
+    int xf_cur = -1;
+    V oo = o, od = d;
     for (uint32_t k = first; k < first + cnt; ++k) {
-      const D* r = W.prim + kWorldRec * k;
+      const PrimRec q = load_rec(pr + kWorldRec * k);
+      const int xf = (int)(q.meta0 >> 8) - 1;
+      if (xf != xf_cur) {
+        xf_cur = xf;
+        oo = o, od = d;
+        if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
+      }
       D t;
       if (MODE == 1) ++nt;
-      if (prim_root(W, r, o, d, time, tmin, t)) accept(h, t, (int)k, (int)meta_of(r)[2], tmin);
+      if (root_obj(q, oo, od, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
     }
   };
   for (;;) {
     if (MODE == 1) ++nv;
-    const D* nd = W.node + kWorldRec * node;
-    const uint32_t* refs = reinterpret_cast<const uint32_t*>(nd + 12);
-    D tn[2];
+    const RTW_CONST float* nd = cn + kNodeWords * node;
+    const uint32_t r0 = __float_as_uint(nd[12]), r1 = __float_as_uint(nd[13]);
+    // {child 0, child 1} lanes: lo - margin and hi + margin per axis
+    const f2 lx = f2{nd[0], nd[6]} - bc(mf), hx = f2{nd[3], nd[9]} + bc(mf);
+    const f2 ly = f2{nd[1], nd[7]} - bc(mf), hy = f2{nd[4], nd[10]} + bc(mf);
+    const f2 lz = f2{nd[2], nd[8]} - bc(mf), hz = f2{nd[5], nd[11]} + bc(mf);
+    const f2 x0 = pfma(lx, ix, ox), x1 = pfma(hx, ix, ox);
+    const f2 y0 = pfma(ly, iy, oy), y1 = pfma(hy, iy, oy);
+    const f2 z0 = pfma(lz, iz, oz), z1 = pfma(hz, iz, oz);
+    const float tmaxf = (D)(float)h.t < h.t ? next_up((float)h.t) : (float)h.t;
+    float tn[2];
     bool hit[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {  // widened slab test, inclusive at the current closest root
-      const D* b = nd + 6 * c;
-      const D x0 = ((b[0] - m) - o.x) * inv.x, x1 = ((b[3] + m) - o.x) * inv.x;
-      const D y0 = ((b[1] - m) - o.y) * inv.y, y1 = ((b[4] + m) - o.y) * inv.y;
-      const D z0 = ((b[2] - m) - o.z) * inv.z, z1 = ((b[5] + m) - o.z) * inv.z;
-      const D n = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), tmin));
-      const D f = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), h.t));
+    for (int c = 0; c < 2; ++c) {
+      const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), fmaxf(fminf(z0[c], z1[c]), tminf));
+      const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), fminf(fmaxf(z0[c], z1[c]), tmaxf));
       tn[c] = n;
       hit[c] = n <= f;
     }
-    const uint32_t r0 = refs[0], r1 = refs[1];
-    if (hit[0] && (r0 & kLeafBit)) leaf(r0);
-    if (hit[1] && (r1 & kLeafBit)) leaf(r1);
-    const bool i0 = hit[0] && !(r0 & kLeafBit), i1 = hit[1] && !(r1 & kLeafBit);
-    if (i0 && i1) {
-      const bool first0 = tn[0] <= tn[1];
-      stack[(sp++) * kWorldBlock] = first0 ? r1 : r0;
+    const bool any0 = __ballot(hit[0]) != 0, any1 = __ballot(hit[1]) != 0;
+    if (any0 && (r0 & kLeafBit)) leaf(r0);
+    if (any1 && (r1 & kLeafBit)) leaf(r1);
+    const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
+    if (i0 && i1) {  // nearer child first by vote of the lanes that hit
+      const uint32_t v0 = (uint32_t)__popcll(__ballot(hit[0] && (!hit[1] || tn[0] <= tn[1])));
+      const uint32_t v1 = (uint32_t)__popcll(__ballot(hit[1] && (!hit[0] || tn[1] < tn[0])));
+      const bool first0 = v0 >= v1;
+      stack[sp++] = first0 ? r1 : r0;
       node = first0 ? r0 : r1;
     } else if (i0) {
       node = r0;
@@ -201,7 +274,7 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
       node = r1;
     } else {
       if (sp == 0) break;
-      node = stack[(--sp) * kWorldBlock];
+      node = stack[--sp];
     }
   }
 }
@@ -269,10 +342,10 @@ __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v
 template <int MODE, int OCC>
 __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + threadIdx.x;
+  uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kBvhStack;  // this wave's stack
   const WorldView W = A.w;  // a local copy: no reference to the by-value argument escapes
   const D margin = A.margin;
-  const uint32_t* order = reinterpret_cast<const uint32_t*>(W.node + kWorldRec * W.n_nodes);
+  const uint32_t* order = W.order;
   const uint32_t lid = lane_id();
   const uint32_t npix = A.t.row_count * A.t.W;
   const uint32_t units_per_tile = kTileW * kTileH * A.t.n_chunks;
@@ -488,7 +561,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   }
 }
 
-size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * kWorldBlock * sizeof(uint32_t); }
+size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * (kWorldBlock / 64) * sizeof(uint32_t); }
 
 template <int OCC>
 static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {

@@ -90,7 +90,7 @@ Box prim_box(const rtw_prim& p, const rtw_xform* xf) {
 }
 
 struct Bvh {
-  std::vector<double> nodes;  // kWorldRec per node
+  std::vector<float> nodes;  // kNodeWords per node
   std::vector<uint32_t> order;  // stored position -> original prim index
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
 };
@@ -119,7 +119,7 @@ class Builder {
   std::vector<std::array<double, 3>> cent_;
 
   uint32_t alloc() {
-    out_.nodes.resize(out_.nodes.size() + rtwk::kWorldRec, 0.0);
+    out_.nodes.resize(out_.nodes.size() + rtwk::kNodeWords, 0.0f);
     return out_.n_nodes++;
   }
   Box range_box(uint32_t b, uint32_t e) const {
@@ -205,10 +205,20 @@ class Builder {
     const uint32_t c0 = m == e ? leaf(b, e) : child(b, m, depth + 1);
     const uint32_t c1 = m == e ? (rtwk::kLeafBit | e) : child(m, e, depth + 1);
     const Box b0 = range_box(b, m), b1 = range_box(m, e);
-    double* nd = out_.nodes.data() + (size_t)rtwk::kWorldRec * n;
+    float* nd = out_.nodes.data() + (size_t)rtwk::kNodeWords * n;
+    auto down = [](double x) {  // largest float <= x
+      float f = (float)x;
+      if ((double)f > x) f = std::nextafter(f, -INFINITY);
+      return f;
+    };
+    auto up = [](double x) {  // smallest float >= x
+      float f = (float)x;
+      if ((double)f < x) f = std::nextafter(f, INFINITY);
+      return f;
+    };
     for (int k = 0; k < 3; ++k) {
-      nd[k] = b0.lo[k], nd[3 + k] = b0.hi[k];
-      nd[6 + k] = b1.lo[k], nd[9 + k] = b1.hi[k];
+      nd[k] = down(b0.lo[k]), nd[3 + k] = up(b0.hi[k]);
+      nd[6 + k] = down(b1.lo[k]), nd[9 + k] = up(b1.hi[k]);
     }
     uint32_t refs[2] = {c0, c1};
     std::memcpy(nd + 12, refs, sizeof(refs));
@@ -281,7 +291,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   }
   // Device records, in stored (leaf) order; `order_dev` maps list index -> stored position.
   const uint32_t n = d->n_prims;
-  std::vector<double> prim((size_t)rtwk::kWorldRec * std::max(n, 1u), 0.0);
+  std::vector<double> prim((size_t)rtwk::kWorldRec * (n + 1), 0.0);  // + a zero padding record (prefetch)
   std::vector<uint32_t> list_to_pos(n);
   for (uint32_t pos = 0; pos < n; ++pos) {
     const uint32_t li = bvh.order[pos];
@@ -348,13 +358,14 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     img[4 * i + 2] = (uint32_t)pix_bytes, img[4 * i + 3] = (uint32_t)(pix_bytes >> 32);
     pix_bytes += (size_t)d->images[i].width * d->images[i].height * 4;
   }
-  // One allocation: prim | xform | tex | mat | perlin | image | pixels | nodes + order
+  // One allocation: prim | xform | tex | mat | perlin | image | pixels | nodes | order
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t o_prim = 0, o_xf = o_prim + al(prim.size() * 8), o_tex = o_xf + al(xf.size() * 8);
   const size_t o_mat = o_tex + al(tex.size() * 8), o_perl = o_mat + al(mat.size() * 8);
   const size_t o_img = o_perl + al(perl.size() * 8), o_pix = o_img + al(img.size() * 4);
   const size_t o_node = o_pix + al(std::max(pix_bytes, (size_t)4));
-  const size_t total = o_node + al(bvh.nodes.size() * 8 + (size_t)std::max(n, 1u) * 4);
+  const size_t o_order = o_node + al(std::max(bvh.nodes.size() * 4, (size_t)4));
+  const size_t total = o_order + al((size_t)std::max(n, 1u) * 4);
   std::vector<unsigned char> host(total, 0);
   std::memcpy(host.data() + o_prim, prim.data(), prim.size() * 8);
   std::memcpy(host.data() + o_xf, xf.data(), xf.size() * 8);
@@ -365,8 +376,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   for (uint32_t i = 0; i < d->n_images; ++i)
     std::memcpy(host.data() + o_pix + ((size_t)img[4 * i + 2] | ((size_t)img[4 * i + 3] << 32)), d->images[i].rgba,
                 (size_t)d->images[i].width * d->images[i].height * 4);
-  if (!bvh.nodes.empty()) std::memcpy(host.data() + o_node, bvh.nodes.data(), bvh.nodes.size() * 8);
-  if (n) std::memcpy(host.data() + o_node + bvh.nodes.size() * 8, list_to_pos.data(), (size_t)n * 4);
+  if (!bvh.nodes.empty()) std::memcpy(host.data() + o_node, bvh.nodes.data(), bvh.nodes.size() * 4);
+  if (n) std::memcpy(host.data() + o_order, list_to_pos.data(), (size_t)n * 4);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     delete w;
@@ -390,7 +401,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.perlin = reinterpret_cast<const double*>(base + o_perl);
   w->view.image = reinterpret_cast<const uint32_t*>(base + o_img);
   w->view.pixels = base + o_pix;
-  w->view.node = reinterpret_cast<const double*>(base + o_node);
+  w->view.node = reinterpret_cast<const float*>(base + o_node);
+  w->view.order = reinterpret_cast<const uint32_t*>(base + o_order);
   w->view.n_prims = n;
   w->view.n_nodes = bvh.n_nodes;
   w->view.n_perlins = d->n_perlins;
@@ -425,8 +437,11 @@ constexpr int kWorldOccDefault = 1;
 // |o - c| + r over every ray origin o (camera or a surface point) and
 // primitive.  Rect roots and the slab arithmetic are accurate to a few u * L.
 // margin = 1e-7 * L with L = 2 * (max |coordinate| of the scene box and the
-// camera) + 1 covers both with a 4x safety factor, so a box that holds a
-// primitive the linear list would accept is never pruned.
+// camera) + 1 covers both with a 4x safety factor.  The kernel evaluates the
+// slabs in packed f32 (t = fma(b, RN(1/d), RN(-RN(o) RN(1/d)))): expressed in
+// space, its rounding is <= 4 u32 (|o| + |b|) <= 2^-22 L (u32 = 2^-24; the
+// f32 bounds are rounded outward), so 2^-20 L more (4x) is added.  A box
+// that holds a primitive the linear list would accept is never pruned.
 double bvh_margin(const rtw_world_s* w, const rtw_camera* cam) {
   double m = 0;
   for (int k = 0; k < 3; ++k) {
@@ -434,7 +449,8 @@ double bvh_margin(const rtw_world_s* w, const rtw_camera* cam) {
     if (std::isfinite(w->bounds.hi[k])) m = std::max(m, std::fabs(w->bounds.hi[k]));
     m = std::max(m, std::fabs(cam->origin[k]) + cam->lens_radius * 2);
   }
-  return 1e-7 * (2.0 * m + 1.0);
+  const double L = 2.0 * m + 1.0;
+  return 1e-7 * L + 0x1p-20 * L;
 }
 
 int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
