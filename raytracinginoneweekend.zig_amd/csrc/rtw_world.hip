@@ -274,7 +274,7 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
       node = r1;
     } else {
       if (sp == 0) break;
-      node = stack[--sp];
+      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);  // uniform: scalar loads
     }
   }
 }

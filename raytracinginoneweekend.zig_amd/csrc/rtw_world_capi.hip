@@ -428,7 +428,11 @@ int rtw_world_bvh_info(rtw_world w, uint32_t info_out[4]) {
 
 namespace {
 
-constexpr int kWorldOccDefault = 1;
+// Default register-allocation target (waves per SIMD) from the A/B on MI355X
+// (DESIGN.md §6.3): 3 waves hide the BVH's dependent node loads and the
+// Cornell box's emission/rect mix; Perlin-textured worlds keep the 2-wave
+// budget because their noise loops spill at 168 VGPRs.
+int world_occ_default(const rtw_world_s* w) { return w->view.n_perlins ? 1 : 3; }
 
 // Widening of every BVH box test.  A computed sphere root deviates from the
 // exact intersection by at most ~sqrt(u * (hb^2 + |a c|)) / a (u = 2^-53; the
@@ -478,10 +482,9 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   a.margin = bvh_margin(w, cam);
   a.counts = reinterpret_cast<unsigned long long*>(wsb + rtw_ws_stats_off(p));
   const size_t lds = rtwk::world_lds_bytes(w->view.n_perlins);
-  // Register-allocation target (RTW_WORLD_OCC development knob; default from
-  // the A/B on MI355X).
+  // Register-allocation target (RTW_WORLD_OCC development knob overrides).
   const char* oc = getenv("RTW_WORLD_OCC");
-  const int occ = (oc && *oc) ? atoi(oc) : kWorldOccDefault;
+  const int occ = (oc && *oc) ? atoi(oc) : world_occ_default(w);
   static int bpc_cache[5] = {0, 0, 0, 0, 0};
   const int oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
   if (bpc_cache[oi] == 0) bpc_cache[oi] = rtwk::world_blocks_per_cu(lds, oi);

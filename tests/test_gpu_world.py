@@ -103,6 +103,23 @@ def test_world_bvh_equals_linear(rtw, W, earth, scene, w, spp):
         assert info["max_depth"] <= 32 and cb["prim_tests"] * 50 < cl["prim_tests"]
 
 
+@pytest.mark.parametrize("scene,w,spp", [(7, 160, 2), (3, 96, 2), (6, 64, 4)])
+def test_world_register_budgets_agree(rtw, W, earth, scene, w, spp, monkeypatch):
+    # the kernel is instantiated per waves-per-SIMD target (1/3/4); the
+    # register budget changes scheduling and spills, never results
+    b = built(W, scene, earth)
+    cam = b.camera()
+    h = rtw.image_height(w, b.settings.aspect)
+    p = params(rtw, b, w, h, spp)
+    outs = []
+    for occ in ("1", "3", "4"):
+        monkeypatch.setenv("RTW_WORLD_OCC", occ)
+        rgb, mean, _, _ = _render_dev(rtw, W, b, cam, p, linear=False)
+        outs.append((rgb, mean))
+    for rgb, mean in outs[1:]:
+        assert (rgb == outs[0][0]).all() and np.array_equal(mean.view(np.uint32), outs[0][1].view(np.uint32))
+
+
 def test_small_worlds_run_linear(rtw, W, earth):
     for scene in (2, 3, 4, 5, 6):
         b = built(W, scene, earth)  # keep the built scene alive: desc points into it
