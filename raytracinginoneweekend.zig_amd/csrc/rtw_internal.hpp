@@ -166,6 +166,7 @@ hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* li
 // Prims are stored in BVH leaf order; `orig` keeps the list index for the
 // reference's tie rule (later object wins).
 constexpr uint32_t kWorldRec = 16;   // doubles per prim / xform / texture record
+constexpr uint32_t kMaxXfOps = 4;    // ops per transform chain (== RTW_MAX_XFORM_OPS)
 constexpr uint32_t kNodeWords = 16;  // 32-bit words per BVH node
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder caps the depth)

@@ -38,7 +38,9 @@ template <typename P>
 __device__ __forceinline__ void to_object(P xf, V& o, V& d) {
   const uint32_t h = (uint32_t)__builtin_bit_cast(uint64_t, (D)xf[0]);
   const uint32_t n = h & 0xFFu;
-  for (uint32_t i = 0; i < n; ++i) {
+#pragma unroll
+  for (uint32_t i = 0; i < kMaxXfOps; ++i) {  // unrolled: o, d stay in registers
+    if (i >= n) break;
     const auto v = xf + 4 + 3 * i;
     if (((h >> (8 + 4 * i)) & 0xFu) == 0u) {
       o = sub(o, mk((D)v[0], (D)v[1], (D)v[2]));
@@ -54,7 +56,10 @@ __device__ __forceinline__ void to_object(P xf, V& o, V& d) {
 }
 __device__ __forceinline__ void to_world(const D* xf, V& p, V& nrm) {
   const uint32_t h = *reinterpret_cast<const uint32_t*>(xf);
-  for (int i = (int)(h & 0xFFu) - 1; i >= 0; --i) {
+  const int n = (int)(h & 0xFFu);
+#pragma unroll
+  for (int i = (int)kMaxXfOps - 1; i >= 0; --i) {
+    if (i >= n) continue;
     const D* v = xf + 4 + 3 * i;
     if (((h >> (8 + 4 * i)) & 0xFu) == 0u) {
       p = add(p, ld3(v));
@@ -88,6 +93,17 @@ __device__ __forceinline__ PrimRec load_rec(P r) {
   return q;
 }
 
+// XY / XZ / YZ rect (hittable.zig:305-331, :364-390, :423-449): k is the
+// rect's constant axis, (a, b) the in-plane axes.
+__device__ __forceinline__ bool rect_root(const D* r, D ok, D oa, D ob, D dk, D da, D db, D tmin, D& t) {
+  const D tt = (r[4] - ok) / dk;
+  if (tt < tmin) return false;
+  const D x = oa + tt * da, y = ob + tt * db;
+  if (x < r[0] || x > r[1] || y < r[2] || y > r[3]) return false;
+  t = tt;
+  return true;
+}
+
 // The primitive's effective root for ray (o, d) in world space: Sphere.hit /
 // MovingSphere.hit root selection (hittable.zig:96-116, :166-187) or the rect
 // plane hit with its containment test (:278-286, :333-341, :388-396).
@@ -111,20 +127,11 @@ __device__ __forceinline__ bool root_obj(const PrimRec& q, const V& o, const V& 
     t = root;
     return !(root < tmin);
   }
-  D ok, oa, ob, dk, da, db;
-  if (kind == 2u) {
-    ok = o.z, oa = o.x, ob = o.y, dk = d.z, da = d.x, db = d.y;
-  } else if (kind == 3u) {
-    ok = o.y, oa = o.x, ob = o.z, dk = d.y, da = d.x, db = d.z;
-  } else {
-    ok = o.x, oa = o.y, ob = o.z, dk = d.x, da = d.y, db = d.z;
-  }
-  const D tt = (r[4] - ok) / dk;
-  if (tt < tmin) return false;
-  const D x = oa + tt * da, y = ob + tt * db;
-  if (x < r[0] || x > r[1] || y < r[2] || y > r[3]) return false;
-  t = tt;
-  return true;
+  // one copy per axis-aligned kind (a select of the axes is turned into a
+  // dynamically indexed stack copy of o and d by the optimiser)
+  if (kind == 2u) return rect_root(r, o.z, o.x, o.y, d.z, d.x, d.y, tmin, t);
+  if (kind == 3u) return rect_root(r, o.y, o.x, o.z, d.y, d.x, d.z, tmin, t);
+  return rect_root(r, o.x, o.y, o.z, d.x, d.y, d.z, tmin, t);
 }
 __device__ __forceinline__ bool prim_root(const WorldView& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
   const int xf = (int)(q.meta0 >> 8) - 1;
@@ -214,41 +221,42 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
   // compared with tmin rounded down and the closest root rounded up.
   const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
   const f2 ix = bc((float)inv.x), iy = bc((float)inv.y), iz = bc((float)inv.z);
-  const f2 ox = bc(-(float)o.x) * ix, oy = bc(-(float)o.y) * iy, oz = bc(-(float)o.z) * iz;
+  // slab t = fma(bound, RN(1/d), RN(-RN(o) RN(1/d)) -/+ RN(m |RN(1/d)|)): the margin is folded
+  // into the per-lane offsets, lower bounds moved down and upper bounds up
   const float mf = (float)m;
+  const float pxo = -(float)o.x * ix[0], pyo = -(float)o.y * iy[0], pzo = -(float)o.z * iz[0];
+  const float mx = mf * fabsf(ix[0]), my = mf * fabsf(iy[0]), mz = mf * fabsf(iz[0]);
+  const float sx = ix[0] < 0.0f ? -1.0f : 1.0f, sy = iy[0] < 0.0f ? -1.0f : 1.0f, sz = iz[0] < 0.0f ? -1.0f : 1.0f;
+  const f2 oxl = bc(pxo - sx * mx), oxh = bc(pxo + sx * mx);
+  const f2 oyl = bc(pyo - sy * my), oyh = bc(pyo + sy * my);
+  const f2 ozl = bc(pzo - sz * mz), ozh = bc(pzo + sz * mz);
   const float tminf = next_down((float)tmin);
+  auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
+  float tmaxf = round_up(h.t);
   const RTW_CONST float* cn = cptr(W.node);
   const RTW_CONST D* pr = cptr(W.prim);
   uint32_t sp = 0, node = 0;  // wave-uniform
   auto leaf = [&](uint32_t ref) {
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & 0xFFu;
-    int xf_cur = -1;
-    V oo = o, od = d;
     for (uint32_t k = first; k < first + cnt; ++k) {
       const PrimRec q = load_rec(pr + kWorldRec * k);
       const int xf = (int)(q.meta0 >> 8) - 1;
-      if (xf != xf_cur) {
-        xf_cur = xf;
-        oo = o, od = d;
-        if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
-      }
+      V oo = o, od = d;
+      if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
       D t;
       if (MODE == 1) ++nt;
       if (root_obj(q, oo, od, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
     }
+    tmaxf = round_up(h.t);
   };
   for (;;) {
     if (MODE == 1) ++nv;
     const RTW_CONST float* nd = cn + kNodeWords * node;
     const uint32_t r0 = __float_as_uint(nd[12]), r1 = __float_as_uint(nd[13]);
-    // {child 0, child 1} lanes: lo - margin and hi + margin per axis
-    const f2 lx = f2{nd[0], nd[6]} - bc(mf), hx = f2{nd[3], nd[9]} + bc(mf);
-    const f2 ly = f2{nd[1], nd[7]} - bc(mf), hy = f2{nd[4], nd[10]} + bc(mf);
-    const f2 lz = f2{nd[2], nd[8]} - bc(mf), hz = f2{nd[5], nd[11]} + bc(mf);
-    const f2 x0 = pfma(lx, ix, ox), x1 = pfma(hx, ix, ox);
-    const f2 y0 = pfma(ly, iy, oy), y1 = pfma(hy, iy, oy);
-    const f2 z0 = pfma(lz, iz, oz), z1 = pfma(hz, iz, oz);
-    const float tmaxf = (D)(float)h.t < h.t ? next_up((float)h.t) : (float)h.t;
+    // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3
+    const f2 x0 = pfma(f2{nd[0], nd[1]}, ix, oxl), x1 = pfma(f2{nd[6], nd[7]}, ix, oxh);
+    const f2 y0 = pfma(f2{nd[2], nd[3]}, iy, oyl), y1 = pfma(f2{nd[8], nd[9]}, iy, oyh);
+    const f2 z0 = pfma(f2{nd[4], nd[5]}, iz, ozl), z1 = pfma(f2{nd[10], nd[11]}, iz, ozh);
     float tn[2];
     bool hit[2];
 #pragma unroll

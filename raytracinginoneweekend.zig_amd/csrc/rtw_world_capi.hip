@@ -216,9 +216,9 @@ class Builder {
       if ((double)f < x) f = std::nextafter(f, INFINITY);
       return f;
     };
-    for (int k = 0; k < 3; ++k) {
-      nd[k] = down(b0.lo[k]), nd[3 + k] = up(b0.hi[k]);
-      nd[6 + k] = down(b1.lo[k]), nd[9 + k] = up(b1.hi[k]);
+    for (int k = 0; k < 3; ++k) {  // {lo0, lo1} and {hi0, hi1} pairs per axis (packed-f32 operands)
+      nd[2 * k] = down(b0.lo[k]), nd[2 * k + 1] = down(b1.lo[k]);
+      nd[6 + 2 * k] = up(b0.hi[k]), nd[7 + 2 * k] = up(b1.hi[k]);
     }
     uint32_t refs[2] = {c0, c1};
     std::memcpy(nd + 12, refs, sizeof(refs));
@@ -429,10 +429,11 @@ int rtw_world_bvh_info(rtw_world w, uint32_t info_out[4]) {
 namespace {
 
 // Default register-allocation target (waves per SIMD) from the A/B on MI355X
-// (DESIGN.md §6.3): 3 waves hide the BVH's dependent node loads and the
-// Cornell box's emission/rect mix; Perlin-textured worlds keep the 2-wave
-// budget because their noise loops spill at 168 VGPRs.
-int world_occ_default(const rtw_world_s* w) { return w->view.n_perlins ? 1 : 3; }
+// (DESIGN.md §6.3): 4 waves hide the BVH's dependent node loads and the
+// Cornell box's emission/rect mix (despite a small spill); Perlin-textured
+// worlds keep the 2-wave budget because their noise loops spill badly.
+static_assert(rtwk::kMaxXfOps == RTW_MAX_XFORM_OPS, "transform chain length");
+int world_occ_default(const rtw_world_s* w) { return w->view.n_perlins ? 1 : 4; }
 
 // Widening of every BVH box test.  A computed sphere root deviates from the
 // exact intersection by at most ~sqrt(u * (hb^2 + |a c|)) / a (u = 2^-53; the
