@@ -241,11 +241,17 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
     for (uint32_t k = first; k < first + cnt; ++k) {
       const PrimRec q = load_rec(pr + kWorldRec * k);
       const int xf = (int)(q.meta0 >> 8) - 1;
-      V oo = o, od = d;
-      if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
       D t;
       if (MODE == 1) ++nt;
-      if (root_obj(q, oo, od, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
+      bool ok;
+      if (xf < 0) {  // separate calls: no copies of (o, d) on the untransformed path
+        ok = root_obj(q, o, d, time, tmin, t);
+      } else {
+        V oo = o, od = d;
+        to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
+        ok = root_obj(q, oo, od, time, tmin, t);
+      }
+      if (ok) accept(h, t, (int)k, (int)q.orig, tmin);
     }
     tmaxf = round_up(h.t);
   };
