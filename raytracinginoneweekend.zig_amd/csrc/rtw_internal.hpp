@@ -182,8 +182,9 @@ struct WorldView {
   const uint8_t* pixels;
   const float* node;
   const uint32_t* order;
-  uint32_t n_prims, n_nodes, n_perlins, pad;
+  uint32_t n_prims, n_nodes, n_perlins, flags;
 };
+constexpr uint32_t kWorldHasSpheres = 1;  // WorldView.flags
 
 struct WorldArgs {
   TraceArgs<double> t;  // MUST stay at offset 0 (kargs<double>()); t.sc unused

@@ -74,23 +74,41 @@ __device__ __forceinline__ void to_world(const D* xf, V& p, V& nrm) {
   }
 }
 
-// The fields of a primitive record the closest-hit test reads (doubles 0-9
+// The fields of a primitive record the closest-hit test reads (doubles 0-10
 // and the meta words), loaded in one place so the linear loop can prefetch
 // the next record (scalar loads through the constant address space) while
 // the current one is tested.
 struct PrimRec {
-  D v[10];
+  D v[11];
   uint32_t meta0, orig;
 };
 template <typename P>
 __device__ __forceinline__ PrimRec load_rec(P r) {
   PrimRec q;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) q.v[i] = r[i];
+  for (int i = 0; i < 11; ++i) q.v[i] = r[i];
   // meta u32 {kind | xform+1 << 8, mat, orig, 0} occupies doubles 14-15
   q.meta0 = (uint32_t)__builtin_bit_cast(uint64_t, (D)r[14]);
   q.orig = (uint32_t)__builtin_bit_cast(uint64_t, (D)r[15]);
   return q;
+}
+
+// A ray in one primitive space with Sphere.hit's `a` = |d|^2 (hittable.zig:97)
+// and ia = RN(1/a): the root divisions run as Markstein div_rn (rtw_math.hpp:
+// RN(x / b) from RN(1 / b), IEEE division outside the normal range), the same
+// bits as x / a.  (Reciprocals for the rect plane divisions measured slower on
+// the Cornell box: three divisions per transform change plus register
+// pressure, against one division per rect.)
+struct RaySp {
+  V o, d;
+  D a, ia;
+};
+__device__ __forceinline__ RaySp ray_space(const V& o, const V& d, uint32_t flags) {
+  RaySp s;
+  s.o = o, s.d = d;
+  s.a = norm2(d);
+  s.ia = (flags & kWorldHasSpheres) ? (D)1 / s.a : (D)0;  // wave-uniform flag
+  return s;
 }
 
 // XY / XZ / YZ rect (hittable.zig:305-331, :364-390, :423-449): k is the
@@ -108,22 +126,27 @@ __device__ __forceinline__ bool rect_root(const D* r, D ok, D oa, D ob, D dk, D 
 // MovingSphere.hit root selection (hittable.zig:96-116, :166-187) or the rect
 // plane hit with its containment test (:278-286, :333-341, :388-396).
 // Returns false when the primitive cannot be hit at t >= tmin; t may be NaN.
-// root_obj: (o, d) already in the primitive's object space.
-__device__ __forceinline__ bool root_obj(const PrimRec& q, const V& o, const V& d, D time, D tmin, D& t) {
+// root_obj: the ray already in the primitive's object space; RCP: use the
+// ray space's a and RN(1/a) (else plain IEEE divisions; same results).
+template <bool RCP>
+__device__ __forceinline__ bool root_obj(const PrimRec& q, const RaySp& s, D time, D tmin, D& t) {
   const D* r = q.v;
+  const V& o = s.o;
+  const V& d = s.d;
   const uint32_t kind = q.meta0 & 0xFFu;
   if (kind <= 1u) {
     V c = mk(r[0], r[1], r[2]);
-    if (kind == 1u) c = add(c, mul(mk(r[3], r[4], r[5]), (time - r[7]) / r[8]));  // hittable.zig:219-221
+    if (kind == 1u)  // hittable.zig:219-221; r[10] = RN(1 / (time1 - time0))
+      c = add(c, mul(mk(r[3], r[4], r[5]), rtwm::div_rn(time - r[7], r[8], r[10])));
     const V oc = sub(o, c);
-    const D a = norm2(d);
+    const D a = RCP ? s.a : norm2(d);
     const D hb = dot(oc, d);
     const D cc = norm2(oc) - r[9];
     const D disc = hb * hb - a * cc;
     if (disc < 0.0) return false;
     const D sq = sqrt(disc);
-    D root = (-hb - sq) / a;
-    if (root < tmin) root = (-hb + sq) / a;
+    D root = RCP ? rtwm::div_rn(-hb - sq, a, s.ia) : (-hb - sq) / a;
+    if (root < tmin) root = RCP ? rtwm::div_rn(-hb + sq, a, s.ia) : (-hb + sq) / a;
     t = root;
     return !(root < tmin);
   }
@@ -136,7 +159,9 @@ __device__ __forceinline__ bool root_obj(const PrimRec& q, const V& o, const V& 
 __device__ __forceinline__ bool prim_root(const WorldView& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
   const int xf = (int)(q.meta0 >> 8) - 1;
   if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
-  return root_obj(q, o, d, time, tmin, t);
+  RaySp s;
+  s.o = o, s.d = d;
+  return root_obj<false>(q, s, time, tmin, t);
 }
 
 // The adjacent f32 toward +inf / -inf (finite or infinite x; NaN kept).
@@ -192,18 +217,19 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
     const RTW_CONST D* pr = cptr(W.prim);
     PrimRec cur = load_rec(pr);  // (a padding record follows the last primitive)
     int xf_cur = -1;             // wave-uniform: the transform the cached object-space ray is for
-    V oo = o, od = d;
+    RaySp s = ray_space(o, d, W.flags);
     for (uint32_t k = 0; k < W.n_prims; ++k) {
       const PrimRec nxt = load_rec(pr + kWorldRec * (k + 1));
       const int xf = (int)(cur.meta0 >> 8) - 1;
       if (xf != xf_cur) {  // consecutive primitives share a chain (a Box's six rects)
         xf_cur = xf;
-        oo = o, od = d;
+        V oo = o, od = d;
         if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
+        s = ray_space(oo, od, W.flags);
       }
       D t;
       if (MODE == 1) ++nt;
-      if (root_obj(cur, oo, od, time, tmin, t)) accept(h, t, (int)k, (int)cur.orig, tmin);
+      if (root_obj<true>(cur, s, time, tmin, t)) accept(h, t, (int)k, (int)cur.orig, tmin);
       cur = nxt;
     }
     return;
@@ -235,6 +261,7 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
   float tmaxf = round_up(h.t);
   const RTW_CONST float* cn = cptr(W.node);
   const RTW_CONST D* pr = cptr(W.prim);
+  const RaySp ws = ray_space(o, d, W.flags);
   uint32_t sp = 0, node = 0;  // wave-uniform
   auto leaf = [&](uint32_t ref) {
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & 0xFFu;
@@ -245,11 +272,12 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
       if (MODE == 1) ++nt;
       bool ok;
       if (xf < 0) {  // separate calls: no copies of (o, d) on the untransformed path
-        ok = root_obj(q, o, d, time, tmin, t);
+        ok = root_obj<true>(q, ws, time, tmin, t);
       } else {
-        V oo = o, od = d;
-        to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
-        ok = root_obj(q, oo, od, time, tmin, t);
+        RaySp s;
+        s.o = o, s.d = d;
+        to_object(cptr(W.xform) + kWorldRec * xf, s.o, s.d);
+        ok = root_obj<false>(q, s, time, tmin, t);
       }
       if (ok) accept(h, t, (int)k, (int)q.orig, tmin);
     }

@@ -304,6 +304,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
         for (int k = 0; k < 3; ++k) r[3 + k] = p.a[3 + k] - p.a[k];  // center1.sub(center0)
         r[7] = p.a[7];
         r[8] = p.a[8] - p.a[7];  // time1 - time0
+        r[10] = 1.0 / r[8];      // its reciprocal (Markstein division in the kernel)
       }
       r[6] = p.a[6];
       r[9] = p.a[6] * p.a[6];  // sphere.radius * sphere.radius
@@ -404,6 +405,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.node = reinterpret_cast<const float*>(base + o_node);
   w->view.order = reinterpret_cast<const uint32_t*>(base + o_order);
   w->view.n_prims = n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (d->prims[i].kind <= RTW_PRIM_MOVING_SPHERE) w->view.flags |= rtwk::kWorldHasSpheres;
   w->view.n_nodes = bvh.n_nodes;
   w->view.n_perlins = d->n_perlins;
   w->info[0] = bvh.n_nodes, w->info[1] = bvh.n_leaves, w->info[2] = bvh.max_depth, w->info[3] = bvh.max_leaf;
