@@ -201,7 +201,19 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
       mat64[8 * i + k] = rec[k];
       mat32[8 * i + k] = (float)rec[k];
     }
-    if (diel) mat32[8 * i + 6] = 1.0f / (float)m.ir;
+    if (diel) {
+      mat32[8 * i + 6] = 1.0f / (float)m.ir;
+      // Schlick's r0^2 (material.zig:87-91) for ratio = RN(1/ir) (front face)
+      // and ir (back face), with the kernel's operations in each precision.
+      for (int f = 0; f < 2; ++f) {
+        const double rd = f == 0 ? mat64[8 * i + 6] : m.ir;
+        const double r0d = (1.0 - rd) / (1.0 + rd);
+        mat64[8 * i + f] = r0d * r0d;
+        const float rf = f == 0 ? mat32[8 * i + 6] : (float)m.ir;
+        const float r0f = (1.0f - rf) / (1.0f + rf);
+        mat32[8 * i + f] = r0f * r0f;
+      }
+    }
     kind[i] = m.kind;
   }
   for (uint32_t g = 0; g < ng; ++g) {
@@ -241,6 +253,12 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   for (uint32_t j = 0; j + 1 < nn; j += 2) {  // static half of a mixed pair: partner's group
     const bool m0 = j >= n_sn, m1 = j + 1 >= n_sn;
     if (!m0 && m1) cull_tg[j / 2] = (cull_tg[j / 2] & 0xFF00u) | (cull_tg[j / 2] >> 8);
+  }
+  // bit 16: both spheres of the pair move along y only (ndc.x == ndc.z == 0):
+  // the kernel's pretest then skips the x and z centre updates.
+  for (uint32_t p = 0; p < nn_pad / 2; ++p) {
+    const float* q = &cull[(size_t)16 * p];
+    if (q[6] == 0.0f && q[7] == 0.0f && q[10] == 0.0f && q[11] == 0.0f) cull_tg[p] |= 1u << 16;
   }
   const float cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
   const float rho = std::nextafter((float)rho_max, INFINITY);

@@ -64,10 +64,10 @@ RTWC_HD LaneConst lane_const(float a, float alpha, float rho_max) { return {-(a 
 RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz, LaneConst lk, float frac, float cx,
                      float cy, float cz, float ndcx, float ndcy, float ndcz, float nr2, bool moving) {
   float ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
-  if (moving) {
-    ocx = std::fma(ndcx, frac, ocx);
+  if (moving) {  // (the kernel skips the updates whose ndc is 0: an exact no-op)
+    if (ndcx != 0.0f) ocx = std::fma(ndcx, frac, ocx);
     ocy = std::fma(ndcy, frac, ocy);
-    ocz = std::fma(ndcz, frac, ocz);
+    if (ndcz != 0.0f) ocz = std::fma(ndcz, frac, ocz);
   }
   const float hb = std::fma(ocz, dz, std::fma(ocy, dy, ocx * dx));
   const float cc = std::fma(ocz, ocz, std::fma(ocy, ocy, std::fma(ocx, ocx, nr2)));

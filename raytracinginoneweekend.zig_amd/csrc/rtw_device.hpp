@@ -65,6 +65,23 @@ __device__ __forceinline__ V3<R> ld3(const __attribute__((address_space(4))) R* 
   return mk(p[0], p[1], p[2]);
 }
 
+// sqrt of the hot path: rtwm::sqrt_rn (same bits as sqrt, fewer instructions)
+// for f64 when VAR has kVarFastSqrt.
+constexpr int kVarFastSqrt = 32768;
+// Dielectric: Schlick's r0^2 for both ratios precomputed in the material
+// record (rtw_capi.hip: doubles 0, 1 of a dielectric; its albedo is unused).
+constexpr int kVarR0Table = 131072;
+// Pretest: pairs flagged y-only (rtw_capi.hip cull_tg bit 16) skip the x/z
+// centre updates.
+constexpr int kVarYOnly = 65536;
+template <typename R, int VAR>
+__device__ __forceinline__ R sqrt_k(R x) {
+  if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
+    return rtwm::sqrt_rn(x);
+  else
+    return sqrt(x);
+}
+
 // ------------------------------------------------------------------ RNG --
 // Counter-based Zig std.Random.SplitMix64: sample (pixel p, sample s) owns the
 // 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its
@@ -181,16 +198,16 @@ __device__ __forceinline__ PairRec ld_pair(const __attribute__((address_space(4)
   for (int i = 0; i < 8; ++i) r.v[i] = t[8 * p + i];
   return r;
 }
-template <bool MOVING>
+// MOVING: 0 static, 1 moving, 2 moving along y only (ndc.x = ndc.z = 0 for
+// both spheres: the x and z updates would add exact zeros).
+template <int MOVING>
 __device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, f2 na, f2 k,
                                         f2 frac) {
   const f2* P = R_.v;
   f2 ocx = ox - P[0], ocy = oy - P[1], ocz = oz - P[2];
-  if constexpr (MOVING) {
-    ocx = pfma(P[3], frac, ocx);
-    ocy = pfma(P[4], frac, ocy);
-    ocz = pfma(P[5], frac, ocz);
-  }
+  if constexpr (MOVING == 1) ocx = pfma(P[3], frac, ocx);
+  if constexpr (MOVING != 0) ocy = pfma(P[4], frac, ocy);
+  if constexpr (MOVING == 1) ocz = pfma(P[5], frac, ocz);
   const f2 hb = pfma(ocz, dz, pfma(ocy, dy, ocx * dx));
   const f2 cc = pfma(ocz, ocz, pfma(ocy, ocy, pfma(ocx, ocx, P[6])));
   return pfma(na, cc, pfma(hb, hb, k));
@@ -314,9 +331,9 @@ __device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], 
 }
 
 // v / |v| with the three divisions done against RN(1/|v|) (rtw_math.hpp div_rn).
-template <typename R>
+template <typename R, int VAR = 0>
 __device__ __forceinline__ V3<R> normalized_rn(V3<R> v) {  // vec.zig:32-39
-  const R n = sqrt(norm2(v));
+  const R n = sqrt_k<R, VAR>(norm2(v));
   if (n == (R)0) return v;
   const R y = (R)1 / n;
   return mk(rtwm::div_rn(v.x, n, y), rtwm::div_rn(v.y, n, y), rtwm::div_rn(v.z, n, y));
@@ -381,8 +398,8 @@ __device__ __forceinline__ bool wide_root(const RTW_CONST double* w, uint32_t me
 // The reference's literal closest-hit loop (hittable.zig:231-244 with
 // Sphere/MovingSphere.hit's root selection), in list order, from LDS tables;
 // used only for lanes that met a NaN in the grouped loops.
-template <typename R, bool F32>
-__device__ __forceinline__ void seq_closest_hit(const SceneView<R>& S, const R* l_sph, const R* l_rad,
+template <typename R, bool F32, typename SV>
+__device__ __forceinline__ void seq_closest_hit(const SV& S, const R* l_sph, const R* l_rad,
                                              const uint32_t* l_meta, const R* l_tg, const uint32_t* l_perm,
                                              const Lane<R>& L, R a, R tmin, R& tmax, int& hit) {
   tmax = (R)__builtin_huge_val();
@@ -490,8 +507,11 @@ struct KStats {
 // +inf and `hit` -1 on entry.  Wave-converged control is NOT required, but the
 // wide-sphere and pretest loops are wave-uniform (scalar-loaded records).
 // VAR: rtw_trace.hip trace_kernel tuning bits (1, 2, 64 are read here).
-template <typename R, bool F32, int MODE, int VAR>
-__device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTables<R>& T, const Lane<R>& L, R tmin,
+// SV: SceneView<R> (a copy in registers) or `const RTW_CONST SceneView<R>`
+// (the kernel argument itself, re-read with scalar loads where used: keeps
+// the scene fields out of the SGPR budget of the rest of the loop).
+template <typename R, bool F32, int MODE, int VAR, typename SV>
+__device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, const Lane<R>& L, R tmin,
                                             R pre_k, uint32_t lid, KStats& st, int& hit, R& tmax) {
   constexpr bool STATS = MODE == 1;
   constexpr bool CULL = !(VAR & 64);  // packed-f32 pretest for narrow spheres
@@ -544,7 +564,7 @@ __device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTabl
         st.disc += 1;
       }
       if (cand) {
-        const R sq = sqrt(disc);
+        const R sq = sqrt_k<R, VAR>(disc);
         R root = rtwm::div_rn(-hb - sq, a, inv_a);
         if (root < tmin) root = rtwm::div_rn(-hb + sq, a, inv_a);
         accept(root, (int)k, (int)(meta >> 20));
@@ -633,8 +653,10 @@ __device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTabl
     const uint32_t np_static = S.n_sn >> 1;  // pairs with two static spheres
     int fr_g = -1;  // phase B: time group of fr_v
     R fr_v = (R)0;
-    for (uint32_t base = 0; base < S.nn; base += 64) {
-      uint32_t sk[2] = {0u, 0u};  // bit 31-r of sk[h]: sphere base+32h+r proven to miss
+    // The pretest of one 64-sphere block: bit 31-r of sk[h] set = sphere
+    // base+32h+r proven to miss.
+    auto pretest_block = [&](uint32_t base, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, uint32_t (&sk)[2]) {
+      sk[0] = sk[1] = 0u;
       uint32_t tgp_cur = ~0u;
       f2 fr2 = bc(0.0f);
 #pragma unroll
@@ -650,14 +672,17 @@ __device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTabl
             tgp_nxt = ctg[p + 1];
             f2 x;
             if (p < np_static) {
-              x = cull_pair<false>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+              x = cull_pair<0>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
             } else {
-              if (tgp != tgp_cur) {  // wave-uniform
-                tgp_cur = tgp;
-                const uint32_t g0 = tgp & 0xFFu, g1 = tgp >> 8;
+              if ((tgp & 0xFFFFu) != tgp_cur) {  // wave-uniform
+                tgp_cur = tgp & 0xFFFFu;
+                const uint32_t g0 = tgp & 0xFFu, g1 = (tgp >> 8) & 0xFFu;
                 fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
               }
-              x = cull_pair<true>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+              if ((VAR & kVarYOnly) != 0 && (tgp >> 16) != 0u)
+                x = cull_pair<2>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+              else
+                x = cull_pair<1>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
             }
             sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.x), 31);
             sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.y), 31);
@@ -667,6 +692,17 @@ __device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTabl
         // fewer than 16 pairs: move sphere r of the chunk to bit 31 - r
         const uint32_t cnt = p1 > p0 ? 2u * (p1 - p0) : 0u;
         sk[h] = cnt == 0u ? 0u : (cnt == 32u ? sk[h] : sk[h] << (32u - cnt));
+      }
+    };
+    for (uint32_t base = 0; base < S.nn; base += 64) {
+      uint32_t sk[2];
+      pretest_block(base, ox, oy, oz, dx, dy, dz, sk);
+      if constexpr ((VAR & 2048) != 0) {  // measurement: the block twice (same image)
+        f2 ox2 = ox, dx2 = dx;
+        asm volatile("" : "+v"(ox2), "+v"(dx2));
+        uint32_t sk2[2];
+        pretest_block(base, ox2, oy, oz, dx2, dy, dz, sk2);
+        asm volatile("" ::"v"(sk2[0]), "v"(sk2[1]));
       }
       const uint32_t rem = S.nn - base;  // real spheres in this block
       const uint32_t v0 = rem >= 32u ? ~0u : ~(~0u >> rem);
@@ -725,7 +761,7 @@ __device__ __forceinline__ void closest_hit(const SceneView<R>& S, const LdsTabl
 // L, given the unit-ball point b3 (Lambertian / Metal; coop_reject).  Returns
 // true when the ray is absorbed (Metal, material.zig:64); else L's ray,
 // attenuation product and depth move to the next segment.
-template <typename R, bool F32>
+template <typename R, bool F32, int VAR = 0>
 __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, int hit, R tmax, uint32_t kind,
                                             const R (&b3)[3]) {
   // Hit record of the winner (hittable.zig:118-128, :189-198).
@@ -749,7 +785,7 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
   // One normalisation per lane: the unit-ball point (Lambertian) or the
   // ray direction (Metal, Dielectric).
   const V3<R> rs = mk(b3[0], b3[1], b3[2]);
-  const V3<R> nv = normalized_rn(kind <= 1u ? rs : L.d);
+  const V3<R> nv = normalized_rn<R, VAR>(kind <= 1u ? rs : L.d);
   const V3<R> ud = nv;
   V3<R> ndir, att;
   bool absorbed = false;
@@ -769,11 +805,16 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
     const R ir = mp[7];
     const R ratio = front ? mp[6] : ir;
     const R cos_t = fmin(dot(mul(ud, (R)-1), normal), (R)1);
-    const R sin_t = sqrt((R)1 - cos_t * cos_t);
+    const R sin_t = sqrt_k<R, VAR>((R)1 - cos_t * cos_t);
     bool refr = false;
     if (ratio * sin_t <= (R)1) {
-      const R r0 = ((R)1 - ratio) / ((R)1 + ratio);
-      const R r1 = r0 * r0;
+      R r1;
+      if constexpr ((VAR & kVarR0Table) != 0) {
+        r1 = front ? mp[0] : mp[1];  // host: RN(RN((1-ratio)/(1+ratio))^2) per ratio
+      } else {
+        const R r0 = ((R)1 - ratio) / ((R)1 + ratio);
+        r1 = r0 * r0;
+      }
       const R x = (R)1 - cos_t;
       const R x2 = x * x;
       const R refl_p = r1 + ((R)1 - r1) * (x * (x2 * x2));  // Zig pow(x, 5.0)
@@ -782,7 +823,7 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
     if (refr) {  // refract (material.zig:116-121)
       const R ct = fmin(dot(mul(ud, (R)-1), normal), (R)1);
       const V3<R> perp = mul(add(ud, mul(normal, ct)), ratio);
-      const V3<R> par = mul(normal, -sqrt(fabs((R)1 - norm2(perp))));
+      const V3<R> par = mul(normal, -sqrt_k<R, VAR>(fabs((R)1 - norm2(perp))));
       ndir = add(perp, par);
     } else {
       ndir = sub(ud, mul(normal, (R)2 * dot(ud, normal)));

@@ -96,4 +96,31 @@ RTW_HD float div_rn(float x, float b, float y) {
   return q1;
 }
 
+// 3. sqrt_rn(x): f64 sqrt exactly as the compiler lowers __builtin_sqrt for
+//    gfx9 (LLVM AMDGPU lowerFSQRTF64: v_rsq_f64, then Goldschmidt refinement
+//    and two FMA residual corrections) without the input scaling (the scale
+//    is 2^0 for x >= 2^-767) and without the +0/+inf select (x finite,
+//    non-zero): for x in [2^-767, DBL_MAX] the same operations on the same
+//    values, hence the same bits (tests/native/gpu_math_check.hip checks it
+//    on the GPU).  Other x take the full builtin.
+RTW_HD double sqrt_rn(double x) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return std::sqrt(x);  // host passes (the kernels' device code is what runs)
+#else
+  if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023), 0)) {
+    RTW_NO_SPECULATE();
+    return __builtin_sqrt(x);
+  }
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = std::fma(-h, g, 0.5);
+  h = std::fma(h, r, h);
+  g = std::fma(g, r, g);
+  double d = std::fma(-g, g, x);
+  g = std::fma(d, h, g);
+  d = std::fma(-g, g, x);
+  return std::fma(d, h, g);
+#endif
+}
+
 }  // namespace rtwm

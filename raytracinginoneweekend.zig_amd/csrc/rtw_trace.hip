@@ -50,8 +50,11 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   CoopSlots* slots = T.slots;
 
   const uint32_t lid = lane_id();
-  const uint32_t npix = A.row_count * A.W;
-  const uint32_t units_per_tile = kTileW * kTileH * A.n_chunks;
+  // VAR bit 10: the loop's kernel-argument fields are re-read where used
+  // (scalar loads through a laundered kernarg pointer) instead of living in
+  // SGPRs for the whole kernel: the SGPR budget is the limit (spills become
+  // v_readlane/v_writelane VALU instructions).
+#define RTW_KA(f) ((VAR & 1024) ? opaque(kargs<R>())->f : A.f)
   const R tmin = A.tmin;
   const R kInf = (R)__builtin_huge_val();
 
@@ -79,29 +82,30 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       uint32_t base2 = 0;
       if (n > rem) {
         uint32_t b = 0;
-        if (lid == 0) b = atomicAdd(A.counter, kBatch);
+        if (lid == 0) b = atomicAdd(RTW_KA(counter), kBatch);
         base2 = __shfl(b, 0);
       }
       if (need) {
         const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
-        if (unit >= A.total_units) {
+        if (unit >= RTW_KA(total_units)) {
           done = true;
         } else {
+          const uint32_t units_per_tile = kTileW * kTileH * RTW_KA(n_chunks);
           const uint32_t tile = unit / units_per_tile;
           const uint32_t r = unit - tile * units_per_tile;
           const uint32_t c = r >> 6;
           const uint32_t l = r & 63u;
-          const uint32_t ty = tile / A.tiles_x;
-          const uint32_t tx = tile - ty * A.tiles_x;
+          const uint32_t ty = tile / RTW_KA(tiles_x);
+          const uint32_t tx = tile - ty * RTW_KA(tiles_x);
           const uint32_t px = tx * kTileW + (l & 7u);
           const uint32_t ly = ty * kTileH + (l >> 3);
-          if (px < A.W && ly < A.row_count) {  // else: padding unit, take another
+          if (px < RTW_KA(W) && ly < RTW_KA(row_count)) {  // else: padding unit, take another
             have_unit = true;
             L.px = px;
             L.ly = ly;
             L.c = c;
-            L.s = c * A.chunk;
-            L.s_end = min(L.s + A.chunk, A.spp);
+            L.s = c * RTW_KA(chunk);
+            L.s_end = min(L.s + RTW_KA(chunk), RTW_KA(spp));
             L.sx = L.sy = L.sz = 0.0;
           }
         }
@@ -133,6 +137,16 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           }
         }
       } else if (ns) {
+        if constexpr ((VAR & 8192) != 0) {  // measurement: sample start twice (same image)
+          Lane<R> L2 = L;
+          asm volatile("" : "+v"(L2.px));
+          R u2, v2, dk2[2];
+          start_sample_uv<R>(kargs<R>(), L2, u2, v2);
+          coop_reject<R, 2, false>(true, L2.rs, dk2, slots, lid);
+          start_sample_ray<R>(kargs<R>(), L2, u2, v2, dk2[0], dk2[1]);
+          asm volatile("" ::"v"(L2.d.x), "v"(L2.d.y), "v"(L2.d.z), "v"(L2.o.x), "v"(L2.o.y), "v"(L2.o.z),
+                       "v"(L2.time), "v"(L2.rs));
+        }
         R u, v, dk[2];
         start_sample_uv<R>(kargs<R>(), L, u, v);
         coop_reject<R, 2, false>(true, L.rs, dk, slots, lid);
@@ -151,14 +165,18 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     int hit = -1;
     R tmax = kInf;
     if (have_ray) {
-      if (L.depth == A.max_depth) {  // rayColor depth == 0 (main.zig:105-108)
+      if (L.depth == RTW_KA(max_depth)) {  // rayColor depth == 0 (main.zig:105-108)
         ended = true;
       } else {
         if (STATS) st.segments++;
         if constexpr (STATS) {
           if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.wave_iters++;
         }
-        closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
+        if constexpr (VAR & 512)  // scene fields re-read from the kernel argument (SGPR budget)
+          closest_hit<R, F32, MODE, VAR>(opaque(kargs<R>())->sc, T, L, RTW_KA(tmin), RTW_KA(pre_k), lid, st,
+                                         hit, tmax);
+        else
+          closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
 
         if (hit < 0) {  // miss: background (main.zig:109-112)
           const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
@@ -177,10 +195,28 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
       const bool nb = shading && kind <= 2u;
       R b3[3] = {(R)0, (R)0, (R)0};
+      if constexpr ((VAR & 4096) != 0) {  // measurement: the unit-ball sampler twice (same image)
+        if (__any(nb)) {
+          uint64_t rs2 = L.rs;
+          asm volatile("" : "+v"(rs2));
+          R c3[3];
+          coop_reject<R, 3, COOP>(nb, rs2, c3, slots, lid);
+          asm volatile("" ::"v"(c3[0]), "v"(c3[1]), "v"(c3[2]), "v"(rs2));
+        }
+      }
       if (__any(nb)) coop_reject<R, 3, COOP>(nb, L.rs, b3, slots, lid);
       RTW_STAMP(7)
+      if constexpr ((VAR & 16384) != 0) {  // measurement: hit record + scatter twice (same image)
+        if (shading) {
+          Lane<R> L2 = L;
+          asm volatile("" : "+v"(L2.o.x));
+          const int e2 = scatter_hit<R, F32, VAR>(T, L2, hit, tmax, kind, b3) ? 1 : 0;
+          asm volatile("" ::"v"(L2.d.x), "v"(L2.d.y), "v"(L2.d.z), "v"(L2.T.x), "v"(L2.T.y), "v"(L2.T.z),
+                       "v"(L2.o.x), "v"(L2.o.y), "v"(L2.o.z), "v"(e2), "v"(L2.rs));
+        }
+      }
       if (shading) {
-        if (scatter_hit<R, F32>(T, L, hit, tmax, kind, b3)) ended = true;
+        if (scatter_hit<R, F32, VAR>(T, L, hit, tmax, kind, b3)) ended = true;
       }
     }
     RTW_STAMP(8)
@@ -189,7 +225,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       have_ray = false;
       if (STATS) st.samples++;
       if (L.s == L.s_end) {  // unit done: publish the chunk sum
-        double* dst = A.partial + ((size_t)L.c * npix + (size_t)L.ly * A.W + L.px) * 3;
+        const uint32_t npix = RTW_KA(row_count) * RTW_KA(W);
+        double* dst = RTW_KA(partial) + ((size_t)L.c * npix + (size_t)L.ly * RTW_KA(W) + L.px) * 3;
         dst[0] = L.sx;
         dst[1] = L.sy;
         dst[2] = L.sz;
@@ -265,6 +302,21 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
 #endif
     case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
     case 8: launch_var<R, F32, 8>(a, grid, lds, s, mode); break;
+    case 516: launch_var<R, F32, 516>(a, grid, lds, s, mode); break;
+    case 1540: launch_var<R, F32, 1540>(a, grid, lds, s, mode); break;
+    case 520: launch_var<R, F32, 520>(a, grid, lds, s, mode); break;
+    case 1544: launch_var<R, F32, 1544>(a, grid, lds, s, mode); break;
+    case 33284: launch_var<R, F32, 33284>(a, grid, lds, s, mode); break;
+    case 66052: launch_var<R, F32, 66052>(a, grid, lds, s, mode); break;
+    case 131588: launch_var<R, F32, 131588>(a, grid, lds, s, mode); break;
+    case 229892: launch_var<R, F32, 229892>(a, grid, lds, s, mode); break;
+    case 197128: launch_var<R, F32, 197128>(a, grid, lds, s, mode); break;
+#ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
+    case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
+    case 516 + 4096: launch_var<R, F32, 516 + 4096>(a, grid, lds, s, mode); break;
+    case 516 + 8192: launch_var<R, F32, 516 + 8192>(a, grid, lds, s, mode); break;
+    case 516 + 16384: launch_var<R, F32, 516 + 16384>(a, grid, lds, s, mode); break;
+#endif
     default: launch_var<R, F32, 0>(a, grid, lds, s, mode); break;
   }
   return hipGetLastError();
@@ -299,7 +351,10 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #ifndef RTW_ISA_QUICK
     RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128)
+#ifdef RTW_MEASURE
+    RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
+#endif
 #undef RTW_OCC_CASE
   }
   return nb > 0 ? nb : 1;
