@@ -21,7 +21,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)                      # raytracinginoneweekend.zig_amd/
 REPO = os.path.dirname(ROOT)
-LIB_PATH = os.path.join(ROOT, "lib", "librtw_hip.so")
+LIB_PATH = os.environ.get("RTW_LIB_PATH") or os.path.join(ROOT, "lib", "librtw_hip.so")  # (override: dev A/B)
 HEADER_PATH = os.path.join(REPO, "include", "rtw_hip.h")
 
 RTW_OK, RTW_EINVAL, RTW_UNSUPPORTED, RTW_EHIP, RTW_ENOMEM, RTW_ENODEV = 0, -1, -2, -3, -4, -5

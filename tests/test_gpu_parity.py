@@ -175,3 +175,36 @@ def test_config2_full_size_rows_and_properties(rtw, oracle, cover):
     # property: mean colour converges (500 spp vs 50 spp differ by noise only)
     lo = gpu_render(rtw, cam, sph, mats, width=W, height=H, spp=50)
     assert np.abs(img.reshape(-1, 3).mean(0) - lo.reshape(-1, 3).mean(0)).max() < 1.0
+
+
+def test_config3_eight_row_shards_assemble_the_full_frame(rtw, oracle, cover):
+    """BASELINE configs[2] (3840x2160, 8 GPUs, rows interleaved, gather to
+    rank 0) rehearsed on one GPU: the 8 ranks' row tiles, assembled the way
+    rank 0 does after the RCCL gather (rtw_amd.shard), equal a 1-GPU render
+    of the same frame bit for bit; sampled rows of it equal the oracle.
+    Reduced spp (the sharding is spp-independent: every sample's RNG is
+    keyed by its global pixel)."""
+    import torch
+    from rtw_amd.device import TorchRenderer
+    from rtw_amd.shard import assemble, max_rows, shard_rows
+
+    sph, mats, cam, osc, ocam = cover
+    W, spp, world = 3840, 2, 8
+    H = rtw.image_height(W, ASPECT)
+    assert H == 2160
+    R = TorchRenderer(sph, mats, 0)
+    full = R.render(cam, rtw.make_params(W, H, spp)).cpu()
+    tiles = []
+    for r in range(world):
+        rb, rs, rc = shard_rows(H, r, world)
+        part = R.render(cam, rtw.make_params(W, H, spp, row_begin=rb, row_stride=rs, row_count=rc)).cpu()
+        t = torch.zeros((max_rows(H, world), W, 3), dtype=torch.uint8)
+        t[:rc] = part
+        tiles.append(t)
+    torch.cuda.synchronize()
+    img = assemble(tiles, H, world)
+    assert torch.equal(img, full)
+    img = img.numpy()
+    for y in (0, 1079, 2159):
+        o, _ = oracle.render_tier_b(osc, ocam, W, H, spp, row_begin=y, row_stride=1, row_count=1)
+        assert_parity(img[y:y + 1], o, f"config3 row {y}")
