@@ -78,6 +78,24 @@ def traffic_per_launch(args, W, H, spp):
     return round(t["traffic_bytes_per_launch"])
 
 
+def valu_issue(args, W, H, spp):
+    """VALU-issue evidence of the same config from the committed PMC passes
+    (profiles/r01/valu_issue.json, tools/gpu_pmc_valu.sh + tools/valu_json.py),
+    else None: the share of SIMD cycles the VALU issues and the VALU
+    instructions per wave-iteration (one bounce segment per lane)."""
+    path = os.path.join(REPO, "profiles", "r01", "valu_issue.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = t.get("config", {})
+    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision):
+        return None
+    return {"busy_frac": t["valu_busy_frac"], "valu_per_wave_iteration": t["valu_per_wave_iteration"],
+            "variant": t.get("variant"), "source": "profiles/r01/valu_issue.json (PMC SQ_ACTIVE_INST_VALU, "
+            "SQ_INSTS_VALU of one launch)"}
+
+
 def cpu_baseline(width, height, spp_sample):
     """Oracle Tier A (the reference's render loop restated: f64, one sequential
     DefaultPrng(42) stream, recursive rayColor) on one core, on the same frame
@@ -308,8 +326,11 @@ def main():
             "flop_per_launch": flops, "segments_per_launch": counts["segments"],
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
-            "note": "megakernel is FP64-VALU + divergence bound; MFMA n/a (no contraction); HBM traffic is "
-                    "~24 B per 32 samples by construction (DESIGN.md §Roofline)",
+            "valu_issue": valu_issue(args, W, H, spp),
+            "note": "megakernel is VALU-issue bound (valu_issue.busy_frac: the VALU issues in ~88 % of SIMD "
+                    "cycles; f64, f32 and integer-multiply wave64 instructions each take ~4 cycles) plus "
+                    "divergence; `achieved` counts only the algorithm's sphere-test flops; MFMA n/a (no "
+                    "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
         }
     else:  # wavefront headline: HBM-bound path queues
         byts = wavefront_bytes(counts, args.precision, rc * W * n_chunks)
