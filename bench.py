@@ -123,8 +123,8 @@ def world_variant(R, torch, scene, steps, warmup):
     default scene, 600x600x200) or 7 (BASELINE configs[4]: globe + 10k
     spheres, BVH, 1200x675x100; synthetic stand-in for the globe texture).
     Timed with HIP events around the world kernel; a counts pass gives the
-    BVH statistics.  Record bytes = 128 B per node visit and per primitive
-    test (the traversal's data movement, served from L2/MALL)."""
+    BVH statistics (node visits and primitive tests per segment, counted per
+    active lane of the wave-cooperative traversal)."""
     from rtw_amd import world as Wd
     earth = Wd.synthetic_world_map()
     b = Wd.BuiltScene(scene, SEED, image=earth if scene in (4, 7) else None)
