@@ -87,7 +87,7 @@ int wf_bpc(int dev, int prec, int kernel, size_t lds) {
 int kernel_variant(uint32_t precision) {
   const char* v = getenv("RTW_VARIANT");
   if (v && *v) return atoi(v);
-  return precision == RTW_PRECISION_F32 ? 8 + 512 + 131072 : 4 + 512 + 32768 + 131072;
+  return precision == RTW_PRECISION_F32 ? 8 + 512 + 131072 + 262144 : 4 + 512 + 32768 + 131072 + 262144;
 }
 
 }  // namespace

@@ -74,6 +74,10 @@ constexpr int kVarR0Table = 131072;
 // Pretest: pairs flagged y-only (rtw_capi.hip cull_tg bit 16) skip the x/z
 // centre updates.
 constexpr int kVarYOnly = 65536;
+// Trace loop rotated so that the lens-disk points of new samples and the
+// unit-ball points of Lambertian / Metal hits come from ONE coop_reject_mixed
+// pass per iteration (rtw_trace.hip).
+constexpr int kVarMergedStart = 262144;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
@@ -321,6 +325,78 @@ __device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], 
 #pragma unroll
         for (int i = 0; i < D; ++i) x[i] = z[i];
         st += (uint64_t)(D * (nextq + jj + 1u)) * kGamma;
+        pending = false;
+      } else {
+        nextq += 1u << lc;
+      }
+    }
+    P = __ballot(pending);
+  }
+}
+
+// coop_reject for a MIX of requests in one converged pass: dim 3 =
+// randomPointInUnitSphere (rand.zig:22-28), dim 2 = randomPointInUnitDisk
+// (rand.zig:30-36), dim 0 = no request.  The rounds are coop_reject's with the
+// dimension carried per pending lane (slot q = dim << 24 | next candidate):
+// every candidate evaluates three draws (SIMT), a disk candidate q of state B
+// uses the first two, at B + (2q + i + 1) * gamma, and the owner advances its
+// state by its own dimension — the same candidate and state as the lane's
+// sequential loop.  x[2] is unspecified for dim 2.  Wave-converged only.
+template <typename R>
+__device__ __forceinline__ bool in_ball_dim(uint32_t dim, R x0, R x1, R x2) {
+  return dim == 3u ? !(x0 * x0 + x1 * x1 + x2 * x2 >= (R)1)   // rand.zig:26
+                   : !(x0 * x0 + x1 * x1 + (R)0 * (R)0 >= (R)1);  // rand.zig:34: vec3(x, y, 0)
+}
+template <typename R>
+__device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R (&x)[3], CoopSlots* slots,
+                                                  uint32_t lid) {
+  bool pending = false;
+  if (dim != 0u) {  // round 0: every requesting lane its own first candidate
+    uint64_t s = st;
+    x[0] = rrange_m11<R>(s);
+    x[1] = rrange_m11<R>(s);
+    const uint64_t s2 = s;
+    x[2] = rrange_m11<R>(s);
+    st = dim == 3u ? s : s2;
+    pending = !in_ball_dim<R>(dim, x[0], x[1], x[2]);
+  }
+  uint64_t P = __ballot(pending);
+  uint32_t nextq = 0;  // candidates are counted from B = st
+  while (P) {
+    const uint32_t m = (uint32_t)__popcll(P);
+    const uint32_t lc = 31u - (uint32_t)__clz((int)(64u / m));  // c = 2^lc, c*m <= 64
+    const uint32_t r = mbcnt64(P);
+    if (pending) {
+      slots->st[r] = st;
+      slots->q[r] = nextq | (dim << 24);
+    }
+    wave_lds_sync();
+    const uint32_t orank = lid >> lc;
+    bool ok = false;
+    R y[3] = {(R)0, (R)0, (R)0};
+    if (orank < m) {
+      const uint32_t qw = slots->q[orank];
+      const uint32_t d = qw >> 24;
+      uint64_t s = slots->st[orank] + (uint64_t)(d * ((qw & 0xFFFFFFu) + (lid & ((1u << lc) - 1u)))) * kGamma;
+      y[0] = rrange_m11<R>(s);
+      y[1] = rrange_m11<R>(s);
+      y[2] = rrange_m11<R>(s);
+      ok = in_ball_dim<R>(d, y[0], y[1], y[2]);
+    }
+    const uint64_t acc = __ballot(ok);
+    wave_lds_sync();  // slots are rewritten next round
+    const uint32_t first = (r << lc) & 63u;  // pending lanes: r*c < 64
+    const uint64_t mine = lc == 6u ? acc : (acc >> first) & ((1ull << (1u << lc)) - 1ull);
+    const uint32_t jj = mine ? (uint32_t)__builtin_ctzll(mine) : 0u;
+    const int src = (int)(first + jj);
+    R z[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) z[i] = __shfl(y[i], src);
+    if (pending) {
+      if (mine) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) x[i] = z[i];
+        st += (uint64_t)(dim * (nextq + jj + 1u)) * kGamma;
         pending = false;
       } else {
         nextq += 1u << lc;

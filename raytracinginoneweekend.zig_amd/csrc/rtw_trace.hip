@@ -70,9 +70,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   KStats st;
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
 
-  for (;;) {
-    RTW_STAMP(5)
-    // ---- 1. take units for lanes that need one (wave-uniform control) ----
+  // ---- take units for lanes that need one (wave-uniform control) ----
+  auto take_units = [&]() {
     const bool need = !have_unit && !done;
     const uint64_t needmask = __ballot(need);
     if (needmask) {
@@ -117,6 +116,97 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
         qnext += n;
       }
     }
+  };
+
+  // A finished sample joins its chunk sum (main.zig:393); a finished unit is
+  // published.  (A miss added its colour; depth limit and absorption add 0.)
+  auto finish_sample = [&]() {
+    L.s++;
+    have_ray = false;
+    if (STATS) st.samples++;
+    if (L.s == L.s_end) {
+      const uint32_t npix = RTW_KA(row_count) * RTW_KA(W);
+      double* dst = RTW_KA(partial) + ((size_t)L.c * npix + (size_t)L.ly * RTW_KA(W) + L.px) * 3;
+      dst[0] = L.sx;
+      dst[1] = L.sy;
+      dst[2] = L.sz;
+      have_unit = false;
+    }
+  };
+  // One closest-hit step for a lane with a live ray (main.zig:103-112).
+  auto bounce = [&](bool& ended, bool& shading, uint32_t& kind, int& hit, R& tmax) {
+    if (L.depth == RTW_KA(max_depth)) {  // rayColor depth == 0 (main.zig:105-108)
+      ended = true;
+      return;
+    }
+    if (STATS) st.segments++;
+    if constexpr (STATS) {
+      if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.wave_iters++;
+    }
+    if constexpr (VAR & 512)  // scene fields re-read from the kernel argument (SGPR budget)
+      closest_hit<R, F32, MODE, VAR>(opaque(kargs<R>())->sc, T, L, RTW_KA(tmin), RTW_KA(pre_k), lid, st, hit,
+                                     tmax);
+    else
+      closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
+    if (hit < 0) {  // miss: background (main.zig:109-112)
+      const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
+      L.sx += (double)col.x;
+      L.sy += (double)col.y;
+      L.sz += (double)col.z;
+      ended = true;
+    } else {
+      kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
+      shading = true;
+    }
+  };
+
+  if constexpr ((VAR & kVarMergedStart) != 0) {
+    // Rotated loop: [take units] -> [u, v of new samples] -> ONE coop pass:
+    // lens-disk points (new samples) + unit-ball points (the Lambertian /
+    // Metal hits of the previous step) -> [scatter; camera rays] -> [closest
+    // hit].  A lane whose path missed starts its next sample in the next
+    // iteration before that iteration's closest hit, as in the default loop;
+    // each sample's draws are in the reference's order.
+    bool shading = false;
+    uint32_t kind = 0;
+    int hit = -1;
+    R tmax = kInf;
+    for (;;) {
+      RTW_STAMP(5)
+      take_units();
+      if (!__any(have_unit)) {
+        if (__all(done)) break;
+        continue;
+      }
+      RTW_STAMP(0)
+      const bool ns = have_unit && !have_ray;
+      R u = (R)0, v = (R)0;
+      if (ns) start_sample_uv<R>(kargs<R>(), L, u, v);
+      RTW_STAMP(1)
+      const uint32_t dim = (shading && kind <= 2u) ? 3u : (ns ? 2u : 0u);
+      R pt[3] = {(R)0, (R)0, (R)0};
+      if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, pt, slots, lid);
+      RTW_STAMP(7)
+      if (shading) {
+        if (scatter_hit<R, F32, VAR>(T, L, hit, tmax, kind, pt)) finish_sample();  // absorbed
+      }
+      if (ns) {
+        start_sample_ray<R>(kargs<R>(), L, u, v, pt[0], pt[1]);
+        have_ray = true;
+      }
+      RTW_STAMP(8)
+      shading = false;
+      hit = -1;
+      tmax = kInf;
+      bool ended = false;
+      if (have_ray) bounce(ended, shading, kind, hit, tmax);
+      RTW_STAMP(3)
+      if (ended) finish_sample();
+    }
+  } else {
+  for (;;) {
+    RTW_STAMP(5)
+    take_units();
     if (!__any(have_unit)) {
       if (__all(done)) break;
       continue;
@@ -164,32 +254,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     uint32_t kind = 0;
     int hit = -1;
     R tmax = kInf;
-    if (have_ray) {
-      if (L.depth == RTW_KA(max_depth)) {  // rayColor depth == 0 (main.zig:105-108)
-        ended = true;
-      } else {
-        if (STATS) st.segments++;
-        if constexpr (STATS) {
-          if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.wave_iters++;
-        }
-        if constexpr (VAR & 512)  // scene fields re-read from the kernel argument (SGPR budget)
-          closest_hit<R, F32, MODE, VAR>(opaque(kargs<R>())->sc, T, L, RTW_KA(tmin), RTW_KA(pre_k), lid, st,
-                                         hit, tmax);
-        else
-          closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
-
-        if (hit < 0) {  // miss: background (main.zig:109-112)
-          const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
-          L.sx += (double)col.x;
-          L.sy += (double)col.y;
-          L.sz += (double)col.z;
-          ended = true;
-        } else {
-          kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
-          shading = true;
-        }
-      }
-    }
+    if (have_ray) bounce(ended, shading, kind, hit, tmax);
     RTW_STAMP(3)
     {
       // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
@@ -220,20 +285,9 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       }
     }
     RTW_STAMP(8)
-    if (ended) {  // (a miss added its colour above; depth limit and absorption add 0)
-      L.s++;
-      have_ray = false;
-      if (STATS) st.samples++;
-      if (L.s == L.s_end) {  // unit done: publish the chunk sum
-        const uint32_t npix = RTW_KA(row_count) * RTW_KA(W);
-        double* dst = RTW_KA(partial) + ((size_t)L.c * npix + (size_t)L.ly * RTW_KA(W) + L.px) * 3;
-        dst[0] = L.sx;
-        dst[1] = L.sy;
-        dst[2] = L.sz;
-        have_unit = false;
-      }
-    }
+    if (ended) finish_sample();
   }
+  }  // default loop
   if (STATS) {
     atomicAdd(A.stats + 0, st.samples);
     atomicAdd(A.stats + 1, st.segments);
@@ -313,6 +367,8 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 197128: launch_var<R, F32, 197128>(a, grid, lds, s, mode); break;
     case 164356: launch_var<R, F32, 164356>(a, grid, lds, s, mode); break;
     case 131592: launch_var<R, F32, 131592>(a, grid, lds, s, mode); break;
+    case 164356 + 262144: launch_var<R, F32, 164356 + 262144>(a, grid, lds, s, mode); break;
+    case 131592 + 262144: launch_var<R, F32, 131592 + 262144>(a, grid, lds, s, mode); break;
 #ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
     case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
     case 516 + 4096: launch_var<R, F32, 516 + 4096>(a, grid, lds, s, mode); break;
@@ -353,7 +409,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #ifndef RTW_ISA_QUICK
     RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736)
 #ifdef RTW_MEASURE
     RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
 #endif
