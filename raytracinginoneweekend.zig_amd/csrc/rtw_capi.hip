@@ -81,13 +81,16 @@ int wf_bpc(int dev, int prec, int kernel, size_t lds) {
 // A/B on MI355X (profiles/r01/ab_defaults.txt): both use scalar
 // sphere records, coop_reject for the unit-ball point, the narrow-sphere
 // pretest, scene fields re-read from the kernel argument (512) and the
-// precomputed Schlick r0^2 (kVarR0Table); f64 at 4 waves/SIMD (128 VGPRs)
+// precomputed Schlick r0^2 (kVarR0Table), the rotated loop with one mixed
+// lens-disk / unit-ball cooperative pass (kVarMergedStart) that also makes the
+// time and dielectric draws (kVarPreDraw); f64 at 4 waves/SIMD (128 VGPRs)
 // with the exact fast sqrt (kVarFastSqrt), f32 at 5 waves/SIMD (96 VGPRs).
 // RTW_VARIANT overrides (development knob).
 int kernel_variant(uint32_t precision) {
   const char* v = getenv("RTW_VARIANT");
   if (v && *v) return atoi(v);
-  return precision == RTW_PRECISION_F32 ? 8 + 512 + 131072 + 262144 : 4 + 512 + 32768 + 131072 + 262144;
+  return precision == RTW_PRECISION_F32 ? 8 + 512 + 131072 + 262144 + 524288
+                                         : 4 + 512 + 32768 + 131072 + 262144 + 524288;
 }
 
 }  // namespace

@@ -78,6 +78,9 @@ constexpr int kVarYOnly = 65536;
 // unit-ball points of Lambertian / Metal hits come from ONE coop_reject_mixed
 // pass per iteration (rtw_trace.hip).
 constexpr int kVarMergedStart = 262144;
+// With kVarMergedStart: the sample's time draw and the dielectric's draw are
+// made inside the same cooperative pass (coop_reject_mixed `raw`).
+constexpr int kVarPreDraw = 524288;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
@@ -336,29 +339,37 @@ __device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], 
 
 // coop_reject for a MIX of requests in one converged pass: dim 3 =
 // randomPointInUnitSphere (rand.zig:22-28), dim 2 = randomPointInUnitDisk
-// (rand.zig:30-36), dim 0 = no request.  The rounds are coop_reject's with the
-// dimension carried per pending lane (slot q = dim << 24 | next candidate):
-// every candidate evaluates three draws (SIMT), a disk candidate q of state B
-// uses the first two, at B + (2q + i + 1) * gamma, and the owner advances its
-// state by its own dimension — the same candidate and state as the lane's
-// sequential loop.  x[2] is unspecified for dim 2.  Wave-converged only.
+// (rand.zig:30-36), dim 1 = the next single draw (the dielectric's, read
+// speculatively: the state is NOT advanced), dim 0 = no request.  The rounds
+// are coop_reject's with the dimension carried per pending lane (slot q =
+// dim << 24 | next candidate): every candidate evaluates three draws (SIMT),
+// a disk candidate q of state B uses the first two, at B + (2q + i + 1) *
+// gamma, and the owner advances its state by its own dimension — the same
+// candidate and state as the lane's sequential loop.  x[2] is unspecified for
+// dim 2.  `raw` returns Random.float of the draw right after the accepted
+// disk candidate (the sample's time draw, main.zig:99, computed as the
+// candidate's spare third draw; the state is not advanced past it) or, for
+// dim 1, of the next draw.  Wave-converged only.
 template <typename R>
 __device__ __forceinline__ bool in_ball_dim(uint32_t dim, R x0, R x1, R x2) {
   return dim == 3u ? !(x0 * x0 + x1 * x1 + x2 * x2 >= (R)1)   // rand.zig:26
                    : !(x0 * x0 + x1 * x1 + (R)0 * (R)0 >= (R)1);  // rand.zig:34: vec3(x, y, 0)
 }
 template <typename R>
-__device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R (&x)[3], CoopSlots* slots,
-                                                  uint32_t lid) {
+__device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R (&x)[3], R& raw,
+                                                  CoopSlots* slots, uint32_t lid) {
   bool pending = false;
   if (dim != 0u) {  // round 0: every requesting lane its own first candidate
     uint64_t s = st;
-    x[0] = rrange_m11<R>(s);
-    x[1] = rrange_m11<R>(s);
+    const R r0 = rnd<R>(s), r1 = rnd<R>(s);
     const uint64_t s2 = s;
-    x[2] = rrange_m11<R>(s);
-    st = dim == 3u ? s : s2;
-    pending = !in_ball_dim<R>(dim, x[0], x[1], x[2]);
+    const R r2 = rnd<R>(s);
+    x[0] = fma(r0, (R)2, (R)-1);  // randomReal(-1, 1) (rrange_m11)
+    x[1] = fma(r1, (R)2, (R)-1);
+    x[2] = fma(r2, (R)2, (R)-1);
+    raw = dim == 1u ? r0 : r2;
+    st = dim == 3u ? s : (dim == 2u ? s2 : st);
+    pending = dim >= 2u && !in_ball_dim<R>(dim, x[0], x[1], x[2]);
   }
   uint64_t P = __ballot(pending);
   uint32_t nextq = 0;  // candidates are counted from B = st
@@ -373,14 +384,15 @@ __device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R 
     wave_lds_sync();
     const uint32_t orank = lid >> lc;
     bool ok = false;
-    R y[3] = {(R)0, (R)0, (R)0};
+    R y[3] = {(R)0, (R)0, (R)0}, yraw = (R)0;
     if (orank < m) {
       const uint32_t qw = slots->q[orank];
       const uint32_t d = qw >> 24;
       uint64_t s = slots->st[orank] + (uint64_t)(d * ((qw & 0xFFFFFFu) + (lid & ((1u << lc) - 1u)))) * kGamma;
       y[0] = rrange_m11<R>(s);
       y[1] = rrange_m11<R>(s);
-      y[2] = rrange_m11<R>(s);
+      yraw = rnd<R>(s);
+      y[2] = fma(yraw, (R)2, (R)-1);
       ok = in_ball_dim<R>(d, y[0], y[1], y[2]);
     }
     const uint64_t acc = __ballot(ok);
@@ -392,10 +404,12 @@ __device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R 
     R z[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) z[i] = __shfl(y[i], src);
+    const R zraw = __shfl(yraw, src);
     if (pending) {
       if (mine) {
 #pragma unroll
         for (int i = 0; i < 3; ++i) x[i] = z[i];
+        raw = zraw;
         st += (uint64_t)(dim * (nextq + jj + 1u)) * kGamma;
         pending = false;
       } else {
@@ -428,16 +442,23 @@ __device__ __forceinline__ void start_sample_uv(const RTW_CONST TraceArgs<R>* Ap
   v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
 }
 // Part 2, after the lens-disk point (rand.zig:30-36, coop_reject<R, 2>).
-template <typename R>
+// PRE: the time draw was made by coop_reject_mixed (`traw`, the draw at
+// state L.rs + gamma): use it and step the state past it.
+template <typename R, bool PRE = false>
 __device__ __forceinline__ void start_sample_ray(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, R u, R v, R dx,
-                                                 R dy) {
+                                                 R dy, R traw = (R)0) {
   const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
   const V3<R> rd = mk(dx * A.lens_radius, dy * A.lens_radius, (R)0 * A.lens_radius);
   const V3<R> cu = ld3(A.cu), cv = ld3(A.cv), org = ld3(A.origin);
   const V3<R> offset = add(mul(cu, rd.x), mul(cv, rd.y));
   L.d = sub(sub(add(add(ld3(A.llc), mul(ld3(A.horizontal), u)), mul(ld3(A.vertical), v)), org), offset);
   L.o = add(org, offset);
-  L.time = rrange<R>(L.rs, A.time0, A.time1);
+  if constexpr (PRE) {
+    L.time = A.time0 + traw * (A.time1 - A.time0);  // rrange (rand.zig:18-20) of the same draw
+    L.rs += kGamma;
+  } else {
+    L.time = rrange<R>(L.rs, A.time0, A.time1);
+  }
   L.T = mk((R)1, (R)1, (R)1);
   L.depth = 0;
   L.skip = -1;
@@ -837,9 +858,11 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
 // L, given the unit-ball point b3 (Lambertian / Metal; coop_reject).  Returns
 // true when the ray is absorbed (Metal, material.zig:64); else L's ray,
 // attenuation product and depth move to the next segment.
-template <typename R, bool F32, int VAR = 0>
+// PRE: the dielectric's draw was made by coop_reject_mixed (`draw`, the draw
+// at state L.rs + gamma); it is consumed only when the reference draws it.
+template <typename R, bool F32, int VAR = 0, bool PRE = false>
 __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, int hit, R tmax, uint32_t kind,
-                                            const R (&b3)[3]) {
+                                            const R (&b3)[3], R draw = (R)0) {
   // Hit record of the winner (hittable.zig:118-128, :189-198).
   const R* sp = T.sph + 8 * hit;
   const uint32_t meta = T.meta[hit];
@@ -894,7 +917,12 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
       const R x = (R)1 - cos_t;
       const R x2 = x * x;
       const R refl_p = r1 + ((R)1 - r1) * (x * (x2 * x2));  // Zig pow(x, 5.0)
-      refr = refl_p < rnd<R>(L.rs);
+      if constexpr (PRE) {
+        refr = refl_p < draw;
+        L.rs += kGamma;
+      } else {
+        refr = refl_p < rnd<R>(L.rs);
+      }
     }
     if (refr) {  // refract (material.zig:116-121)
       const R ct = fmin(dot(mul(ud, (R)-1), normal), (R)1);

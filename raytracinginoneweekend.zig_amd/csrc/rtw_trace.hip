@@ -183,15 +183,17 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       R u = (R)0, v = (R)0;
       if (ns) start_sample_uv<R>(kargs<R>(), L, u, v);
       RTW_STAMP(1)
-      const uint32_t dim = (shading && kind <= 2u) ? 3u : (ns ? 2u : 0u);
-      R pt[3] = {(R)0, (R)0, (R)0};
-      if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, pt, slots, lid);
+      // dim: 3 unit ball (Lambertian, Metal), 1 the dielectric's draw, 2 lens disk (+ time)
+      constexpr bool PRE = (VAR & kVarPreDraw) != 0;
+      const uint32_t dim = shading ? (kind <= 2u ? 3u : (PRE ? 1u : 0u)) : (ns ? 2u : 0u);
+      R pt[3] = {(R)0, (R)0, (R)0}, raw = (R)0;
+      if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, pt, raw, slots, lid);
       RTW_STAMP(7)
       if (shading) {
-        if (scatter_hit<R, F32, VAR>(T, L, hit, tmax, kind, pt)) finish_sample();  // absorbed
+        if (scatter_hit<R, F32, VAR, PRE>(T, L, hit, tmax, kind, pt, raw)) finish_sample();  // absorbed
       }
       if (ns) {
-        start_sample_ray<R>(kargs<R>(), L, u, v, pt[0], pt[1]);
+        start_sample_ray<R, PRE>(kargs<R>(), L, u, v, pt[0], pt[1], raw);
         have_ray = true;
       }
       RTW_STAMP(8)
@@ -369,6 +371,8 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 131592: launch_var<R, F32, 131592>(a, grid, lds, s, mode); break;
     case 164356 + 262144: launch_var<R, F32, 164356 + 262144>(a, grid, lds, s, mode); break;
     case 131592 + 262144: launch_var<R, F32, 131592 + 262144>(a, grid, lds, s, mode); break;
+    case 426500 + 524288: launch_var<R, F32, 426500 + 524288>(a, grid, lds, s, mode); break;
+    case 393736 + 524288: launch_var<R, F32, 393736 + 524288>(a, grid, lds, s, mode); break;
 #ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
     case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
     case 516 + 4096: launch_var<R, F32, 516 + 4096>(a, grid, lds, s, mode); break;
@@ -409,7 +413,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #ifndef RTW_ISA_QUICK
     RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024)
 #ifdef RTW_MEASURE
     RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
 #endif
