@@ -112,9 +112,19 @@ def cpu_baseline(width, height, spp_sample):
         cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         cpu = "unknown"
-    return {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
-                      f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
+    res = {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
+                     f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
+    # Beside it: the GPU's own contract (Tier B, counter RNG, pixels independent)
+    # on the box's CPU share (16 threads, OpenMP over rows) — context only.
+    threads = 16
+    t0 = time.perf_counter()
+    _, stb = O.render_tier_b(sc, cam, width, height, 2 * spp_sample, DEPTH, threads=threads)
+    dtb = time.perf_counter() - t0
+    res["multicore"] = {"value": round(stb["samples"] / dtb / 1e6, 3), "unit": "Msamples/s", "cores": threads,
+                        "kind": "port (oracle Tier B, OpenMP over rows)",
+                        "sample": f"{width}x{height}x{2 * spp_sample} spp, {stb['samples']} samples in {dtb:.1f} s"}
+    return res
 
 
 def world_variant(R, torch, scene, steps, warmup):

@@ -81,6 +81,8 @@ constexpr int kVarMergedStart = 262144;
 // With kVarMergedStart: the sample's time draw and the dielectric's draw are
 // made inside the same cooperative pass (coop_reject_mixed `raw`).
 constexpr int kVarPreDraw = 524288;
+// Unit refill: each 64-unit batch's (tile, chunk) decoded once per batch.
+constexpr int kVarBatchDecode = 1048576;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)

@@ -10,9 +10,12 @@
 //    lane that finishes its unit takes the next one from the wave's batch at
 //    once ("lane-level regeneration"), so lanes never wait for the slowest
 //    path of the wave and the end-of-launch drain is one chunk long.
-//  * Per lane, one loop iteration = [take a unit] -> [start a sample: seed the
-//    per-sample Xoshiro256++, camera ray] -> [one bounce segment].  Paths of
-//    different length share the wave without padding to the longest.
+//  * Per lane, one loop iteration = [take a unit] -> [start a sample: the
+//    sample's counter-RNG block, camera ray] -> [one bounce segment].  Paths
+//    of different length share the wave without padding to the longest.  The
+//    default variant rotates the iteration so that the lens-disk points of the
+//    new samples and the unit-ball points of the hits come from ONE
+//    cooperative rejection pass (kVarMergedStart, below).
 //  * The closest-hit loop over the sphere list is wave-UNIFORM: every lane
 //    tests sphere k at the same time, so sphere k's record is fetched with
 //    scalar loads (s_load, SGPR operands of the VALU ops): zero VGPRs and zero
@@ -36,7 +39,12 @@ namespace rtwk {
 // 4 waves per SIMD (VGPR budget 128); bit3 = 5 waves per SIMD (budget 96);
 // bit4 = per-lane rejection loops instead of coop_reject; bit5 = coop_reject
 // for the lens disk too; bit6 = no narrow-sphere pretest (every lane tests
-// every sphere exactly).
+// every sphere exactly); bit9 (512) = scene fields re-read from the kernel
+// argument; bit10 (1024) = the loop's other argument fields too; bits 11-14 =
+// phase-duplication measurement builds (RTW_MEASURE); rtw_device.hpp: 32768
+// kVarFastSqrt, 65536 kVarYOnly, 131072 kVarR0Table, 262144 kVarMergedStart,
+// 524288 kVarPreDraw, 1048576 kVarBatchDecode.  Defaults: rtw_capi.hip
+// kernel_variant; A/B tables: profiles/r01/ab_*.txt.
 template <typename R, bool F32, int MODE, int VAR>
 __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 1)) trace_kernel(TraceArgs<R> A) {
   constexpr bool STATS = MODE == 1;
@@ -70,6 +78,17 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   KStats st;
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
 
+  // (tile x, tile y, chunk) of the wave's current unit batch and of a newly
+  // fetched one (VAR kVarBatchDecode; wave-uniform).
+  uint32_t cur_tx = 0, cur_ty = 0, cur_c = 0, nb_tx = 0, nb_ty = 0, nb_c = 0;
+  auto decode_batch = [&](uint32_t base, uint32_t& tx, uint32_t& ty, uint32_t& c) {
+    const uint32_t b64 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 6));
+    const uint32_t nc = RTW_KA(n_chunks), txs = RTW_KA(tiles_x);
+    const uint32_t tile = b64 / nc;
+    c = b64 - tile * nc;
+    ty = tile / txs;
+    tx = tile - ty * txs;
+  };
   // ---- take units for lanes that need one (wave-uniform control) ----
   auto take_units = [&]() {
     const bool need = !have_unit && !done;
@@ -84,18 +103,31 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
         if (lid == 0) b = atomicAdd(RTW_KA(counter), kBatch);
         base2 = __shfl(b, 0);
       }
+      if constexpr ((VAR & kVarBatchDecode) != 0) {
+        // A batch is 64 aligned units = one (tile, chunk): decoded once per
+        // batch (wave-uniform) instead of two integer divisions per refill.
+        if (n > rem) decode_batch(base2, nb_tx, nb_ty, nb_c);
+      }
       if (need) {
         const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
         if (unit >= RTW_KA(total_units)) {
           done = true;
         } else {
-          const uint32_t units_per_tile = kTileW * kTileH * RTW_KA(n_chunks);
-          const uint32_t tile = unit / units_per_tile;
-          const uint32_t r = unit - tile * units_per_tile;
-          const uint32_t c = r >> 6;
-          const uint32_t l = r & 63u;
-          const uint32_t ty = tile / RTW_KA(tiles_x);
-          const uint32_t tx = tile - ty * RTW_KA(tiles_x);
+          uint32_t tx, ty, c;
+          const uint32_t l = unit & 63u;
+          if constexpr ((VAR & kVarBatchDecode) != 0) {
+            const bool in_cur = rank < rem;
+            tx = in_cur ? cur_tx : nb_tx;
+            ty = in_cur ? cur_ty : nb_ty;
+            c = in_cur ? cur_c : nb_c;
+          } else {
+            const uint32_t units_per_tile = kTileW * kTileH * RTW_KA(n_chunks);
+            const uint32_t tile = unit / units_per_tile;
+            const uint32_t r = unit - tile * units_per_tile;
+            c = r >> 6;
+            ty = tile / RTW_KA(tiles_x);
+            tx = tile - ty * RTW_KA(tiles_x);
+          }
           const uint32_t px = tx * kTileW + (l & 7u);
           const uint32_t ly = ty * kTileH + (l >> 3);
           if (px < RTW_KA(W) && ly < RTW_KA(row_count)) {  // else: padding unit, take another
@@ -112,6 +144,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if (n > rem) {
         qnext = base2 + (n - rem);
         qend = base2 + kBatch;
+        if constexpr ((VAR & kVarBatchDecode) != 0) cur_tx = nb_tx, cur_ty = nb_ty, cur_c = nb_c;
       } else {
         qnext += n;
       }
@@ -373,6 +406,8 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 131592 + 262144: launch_var<R, F32, 131592 + 262144>(a, grid, lds, s, mode); break;
     case 426500 + 524288: launch_var<R, F32, 426500 + 524288>(a, grid, lds, s, mode); break;
     case 393736 + 524288: launch_var<R, F32, 393736 + 524288>(a, grid, lds, s, mode); break;
+    case 950788 + 1048576: launch_var<R, F32, 950788 + 1048576>(a, grid, lds, s, mode); break;
+    case 918024 + 1048576: launch_var<R, F32, 918024 + 1048576>(a, grid, lds, s, mode); break;
 #ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
     case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
     case 516 + 4096: launch_var<R, F32, 516 + 4096>(a, grid, lds, s, mode); break;
@@ -413,7 +448,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #ifndef RTW_ISA_QUICK
     RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024) RTW_OCC_CASE(1999364) RTW_OCC_CASE(1966600)
 #ifdef RTW_MEASURE
     RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
 #endif
