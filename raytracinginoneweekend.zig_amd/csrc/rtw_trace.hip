@@ -409,6 +409,8 @@ static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds,
     case 950788 + 1048576: launch_var<R, F32, 950788 + 1048576>(a, grid, lds, s, mode); break;
     case 918024 + 1048576: launch_var<R, F32, 918024 + 1048576>(a, grid, lds, s, mode); break;
     case 950792: launch_var<R, F32, 950792>(a, grid, lds, s, mode); break;
+    case 950788 + 65536: launch_var<R, F32, 950788 + 65536>(a, grid, lds, s, mode); break;
+    case 950788 + 65536 + 1048576: launch_var<R, F32, 950788 + 65536 + 1048576>(a, grid, lds, s, mode); break;
     case 918020: launch_var<R, F32, 918020>(a, grid, lds, s, mode); break;
 #ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
     case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
@@ -450,7 +452,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var) {
 #ifndef RTW_ISA_QUICK
     RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
 #endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024) RTW_OCC_CASE(1999364) RTW_OCC_CASE(1966600) RTW_OCC_CASE(950792) RTW_OCC_CASE(918020)
+    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024) RTW_OCC_CASE(1999364) RTW_OCC_CASE(1966600) RTW_OCC_CASE(950792) RTW_OCC_CASE(918020) RTW_OCC_CASE(1016324) RTW_OCC_CASE(2064900)
 #ifdef RTW_MEASURE
     RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
 #endif
