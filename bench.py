@@ -257,9 +257,17 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (no CPU fallback)")
+    # Rehearsal knobs (N > 1 on a box with fewer GPUs; never used by the
+    # driver): RTW_DIST_BACKEND=gloo, RTW_SHARE_GPU=1 (rank r on GPU r mod count).
+    backend = os.environ.get("RTW_DIST_BACKEND", "nccl")
+    if os.environ.get("RTW_SHARE_GPU"):
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     W = args.width
     H = R.image_height(W, ASPECT)

@@ -44,8 +44,11 @@ def gather_image(local: torch.Tensor, height: int, rank: int, world: int, group=
     tile[: local.shape[0]] = local
     if world == 1:
         return assemble([tile], height, 1)
+    dev = tile.device
+    if tile.is_cuda and dist.get_backend(group) == "gloo":  # gloo gathers host tensors only
+        tile = tile.cpu()
     gl = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
     dist.gather(tile, gather_list=gl, dst=0, group=group)
     if rank != 0:
         return None
-    return assemble(gl, height, world)
+    return assemble(gl, height, world).to(dev)
