@@ -96,6 +96,22 @@ def valu_issue(args, W, H, spp):
             "SQ_INSTS_VALU of one launch)"}
 
 
+def wf_traffic(args, W, H, rc, spp):
+    """HBM bytes of one wavefront frame (every wf_extend + wf_shade launch) from
+    the committed PMC passes of the same config (profiles/r01/wf_traffic.json,
+    tools/gpu_pmc_wf.sh), else None."""
+    path = os.path.join(REPO, "profiles", "r01", "wf_traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = t.get("config", {})
+    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision) \
+            or rc != H or args.wf_paths not in (0,):
+        return None
+    return round(t["traffic_bytes_per_frame"])
+
+
 def cpu_baseline(width, height, spp_sample):
     """Oracle Tier A (the reference's render loop restated: f64, one sequential
     DefaultPrng(42) stream, recursive rayColor) on one core, on the same frame
@@ -234,7 +250,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
                          "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
                          "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts},
             "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
@@ -354,7 +370,7 @@ def main():
         byts = wavefront_bytes(counts, args.precision, rc * W * n_chunks)
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
                     "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
                     "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,
                     "valu": {"achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",

@@ -1,5 +1,6 @@
 """One render of BASELINE configs[1] per precision, for rocprofv3 (kernel
-trace / PMC passes).  Usage: python tools/prof_run.py [f64|f32|both] [reps]"""
+trace / PMC passes).  Usage: python tools/prof_run.py [f64|f32|both|wf64] [reps]
+(wf64: the same frame on the wavefront engine, BASELINE configs[3])"""
 import os
 import sys
 
@@ -21,7 +22,10 @@ def main():
     cam = R.cover_camera(16 / 9)
     rend = TorchRenderer(sph, mats, 0)
     for prec in (["f64", "f32"] if which == "both" else [which]):
-        p = R.make_params(W, H, spp, precision=prec)
+        if prec == "wf64":
+            p = R.make_params(W, H, spp, precision="f64", engine="wavefront")
+        else:
+            p = R.make_params(W, H, spp, precision=prec)
         for _ in range(reps):
             rend.render(cam, p)
         torch.cuda.synchronize()

@@ -1,0 +1,41 @@
+"""HBM traffic of one wavefront frame (wf_extend + wf_shade, every bounce
+launch of the frame) from the FETCH_SIZE / WRITE_SIZE PMC passes of
+tools/gpu_pmc_wf.sh -> profiles/<tag>/wf_traffic.json, read by bench.py for
+wavefront_variant.roofline.traffic.  FETCH_SIZE is doubled (gfx950 tallies
+128-B reads at 64 B, MI355X_MICROARCH.md §HBM); units are KB (rocprofv3).
+Usage: python tools/wf_traffic_json.py FETCH_DIR WRITE_DIR OUT [frames]"""
+import csv
+import glob
+import json
+import sys
+
+fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
+frames = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+KERNELS = ("wf_extend", "wf_shade")
+
+
+def total(d, name):
+    v, per = 0.0, {}
+    for f in glob.glob(f"{d}/*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+            if k and r["Counter_Name"] == name:
+                x = float(r["Counter_Value"])
+                v += x
+                per[k] = per.get(k, 0.0) + x
+    return v, per
+
+
+fk, fper = total(fetch_dir, "FETCH_SIZE")
+wk, wper = total(write_dir, "WRITE_SIZE")
+if fk == 0 or wk == 0:
+    sys.exit("no wf_extend / wf_shade counter rows")
+res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", "engine": "wavefront"},
+       "fetch_size_kb_per_frame": fk / frames, "write_size_kb_per_frame": wk / frames,
+       "per_kernel_bytes_per_frame": {k: (2 * fper.get(k, 0.0) + wper.get(k, 0.0)) * 1024 / frames for k in KERNELS},
+       "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
+       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one 1200x675x500 f64 "
+                 "wavefront render (tools/prof_run.py wf64); bytes = 2*FETCH_SIZE + WRITE_SIZE (KB x 1024), "
+                 "summed over every wf_extend and wf_shade launch of the frame"}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
