@@ -63,3 +63,12 @@ def test_cpu_baseline_is_bounded_and_stated():
     cb = load("bench.json")["cpu_baseline"]
     assert cb["unit"] == "Msamples/s" and cb["cores"] == 1 and cb["kind"] in ("port", "reference")
     assert cb["value"] > 0 and "spp" in cb["sample"]
+
+
+def test_wavefront_traffic_is_the_pmc_measurement():
+    wf = load("bench.json")["wavefront_variant"]["roofline"]
+    t = load("wf_traffic.json")
+    assert wf["traffic"] == round(t["traffic_bytes_per_frame"])
+    # the queues move close to their algorithmic bytes (no wasted re-reads)
+    assert 0.8 < wf["traffic"] / wf["algorithmic_bytes_per_frame"] < 1.5
+    assert abs(wf["frac"] - wf["achieved"] / wf["peak"]) < 1e-3
