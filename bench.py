@@ -107,7 +107,7 @@ def wf_traffic(args, W, H, rc, spp):
         return None
     c = t.get("config", {})
     if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision) \
-            or rc != H or args.wf_paths not in (0,):
+            or rc != H or args.wf_paths != 0:
         return None
     return round(t["traffic_bytes_per_frame"])
 
@@ -207,11 +207,15 @@ def wavefront_bytes(counts, precision, units):
     bounce segment, extend reads o, d, time (+ the skip word in f32) and
     writes (root, winner); shade reads the path + (root, winner) and writes
     the path.  Per sample: the home slot's unit, sample index and f64x3 sum
-    (read + write).  Per unit: the f64x3 chunk sum."""
+    (read + write).  Per unit: the f64x3 chunk sum.  `counts` is the
+    wavefront engine's own counts pass: segments traced by the in-register
+    drain (wf_finish, counts["drain_segments"]) move no queue bytes (its one
+    load of each live path, <= 96 B x slots, is left out: < 0.1 %)."""
     r = 8 if precision == "f64" else 4
     path = 10 * r + 8 + 4 + 4
     seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
-    return counts["segments"] * seg + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
+    queued = counts["segments"] - counts.get("drain_segments", 0)
+    return queued * seg + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
 
 
 def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, samples_all, world, rank, dist,
@@ -221,6 +225,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     path queues stream through HBM every bounce)."""
     p = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
                       precision=args.precision, engine="wavefront", wf_paths=args.wf_paths)
+    counts = rend.counts(cam, p)  # untimed: the queue / in-register split of the segments
     for _ in range(max(1, args.warmup)):
         rend.render(cam, p, out=out)
     torch.cuda.synchronize()
@@ -247,12 +252,14 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     units = rc * W * ((spp + chunk - 1) // chunk)
     byts = wavefront_bytes(counts, args.precision, units)
     gbs = byts / (ms * 1e-3) / 1e9
+    drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
-                         "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
-                         "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts},
+                         "kernel": "wf_extend + wf_shade (all bounce launches of one frame) + wf_finish",
+                         "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts,
+                         "drain_segment_frac": round(drain, 4)},
             "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
                     "same Tier-B image as the megakernel, bit for bit"}
 
@@ -367,11 +374,11 @@ def main():
                     "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
         }
     else:  # wavefront headline: HBM-bound path queues
-        byts = wavefront_bytes(counts, args.precision, rc * W * n_chunks)
+        byts = wavefront_bytes(rend.counts(cam, params), args.precision, rc * W * n_chunks)
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
-                    "kernel": "wf_extend + wf_shade (all bounce launches of one frame)",
+                    "kernel": "wf_extend + wf_shade (all bounce launches of one frame) + wf_finish",
                     "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,
                     "valu": {"achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                              "frac": round(achieved_tf / peak, 4)}}

@@ -167,6 +167,12 @@ int rtw_render_device(rtw_scene scene, const rtw_camera *cam, const rtw_params *
  * count samples and segments (the wavefront engine in its shade kernel). */
 int rtw_render_counts(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                       void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
+/* The same pass with counts_out[6]: the four above, then the segments traced
+ * and the samples finished by the wavefront engine's in-register drain
+ * (wf_finish: paths that no longer stream through the HBM queues; 0 for the
+ * megakernel and with RTW_WF_FINISH=0). */
+int rtw_render_counts_ex(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
+                         void *workspace, size_t workspace_bytes, uint64_t counts_out[6]);
 
 /* =================================================== general worlds ===
  * Every other scene of the reference (main.zig:123-290) and BASELINE.json

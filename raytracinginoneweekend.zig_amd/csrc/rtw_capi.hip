@@ -479,6 +479,9 @@ struct WfLaunch<double> {
   static hipError_t shd(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_shade_f64(a, g, l, s, stats);
   }
+  static hipError_t fin(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_finish_f64(a, g, l, s, stats);
+  }
 };
 template <>
 struct WfLaunch<float> {
@@ -490,6 +493,9 @@ struct WfLaunch<float> {
   }
   static hipError_t shd(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_shade_f32(a, g, l, s, stats);
+  }
+  static hipError_t fin(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_finish_f32(a, g, l, s, stats);
   }
 };
 
@@ -521,7 +527,8 @@ uint32_t* poll_words() {
 // Wavefront render: generate, then batches of kWfIters (extend, shade)
 // pairs; after each batch wf_count sums the segment counts of queue A and the
 // total is copied to pinned memory.  The host stops once a batch (checked one
-// batch behind, so the GPU never idles on the poll) left the queue empty.
+// batch behind, so the GPU never idles on the poll) left the queue empty, or
+// hands the drain to wf_finish once the live count shows retiring slots.
 // Empty batches cost only the launches: every wave reads its count first.
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
@@ -583,6 +590,11 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   const char* tos = getenv("RTW_WF_TIMEOUT_S");
   const double timeout_s = (tos && *tos) ? atof(tos) : 300.0;
   const auto t_start = std::chrono::steady_clock::now();
+  // Drain in registers (wf_finish) once the polled live count falls below
+  // RTW_WF_FINISH x slots (default 1: as soon as slots start to retire, i.e.
+  // the unit queue ran dry; 0 = drain through the queues to the end).
+  const char* fe = getenv("RTW_WF_FINISH");
+  const double fin_frac = (fe && *fe) ? atof(fe) : 1.0;
   int st = RTW_OK;
   for (uint64_t batch = 0;; ++batch) {
     for (int k = 0; k < kWfIters && st == RTW_OK; ++k) {
@@ -605,7 +617,15 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
         st = fail(RTW_EHIP, "wavefront batch failed on the device");
         break;
       }
-      if (poll[(batch - 1) & 1] == 0u) break;
+      const uint32_t live = poll[(batch - 1) & 1];
+      if (live == 0u) break;
+      if ((double)live < fin_frac * (double)n) {  // queue A holds the paths after this batch
+        a.in = qa;
+        a.seg_in = seg_a;
+        if ((e = WfLaunch<R>::fin(a, max_grid, lds, stream, stats)) != hipSuccess)
+          st = fail(RTW_EHIP, "wavefront finish launch: %s", hipGetErrorString(e));
+        break;
+      }
     }
     if (batch > max_batches ||
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s) {
@@ -729,8 +749,8 @@ int rtw_render_device(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   return launch_all(sc, cam, p, workspace, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, 0);
 }
 
-int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
-                      size_t ws_bytes, uint64_t counts_out[4]) {
+int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
+                         size_t ws_bytes, uint64_t counts_out[6]) {
   if (!sc || !cam || !counts_out) return fail(RTW_EINVAL, "scene/camera/counts is NULL");
   const int v = validate(p);
   if (v != RTW_OK) return v;
@@ -762,7 +782,19 @@ int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   counts_out[2] = st[1] * sc->n_static;
   counts_out[3] = st[1] * sc->n_moving;
   if (p->precision == RTW_PRECISION_F32) counts_out[2] -= st[2];
+  counts_out[4] = st[9];  // wf_finish (rtw_wavefront.hip shade_step FIN)
+  counts_out[5] = st[10];
   return RTW_OK;
+}
+
+int rtw_render_counts(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
+                      size_t ws_bytes, uint64_t counts_out[4]) {
+  if (!counts_out) return fail(RTW_EINVAL, "scene/camera/counts is NULL");
+  uint64_t c[6];
+  const int r = rtw_render_counts_ex(sc, cam, p, workspace, ws_bytes, c);
+  if (r == RTW_OK)
+    for (int i = 0; i < 4; ++i) counts_out[i] = c[i];
+  return r;
 }
 
 int rtw_render(const rtw_camera* cam, const rtw_sphere* spheres, uint32_t n, const rtw_material* mats, uint32_t nm,

@@ -141,6 +141,8 @@ hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t grid, size_t ld
 hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
 hipError_t launch_wf_extend_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
 hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_wf_finish_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 // Resident workgroups per CU of a bounce kernel (1 = extend, 2 = shade): the
 // persistent grid of that kernel is CUs x this.
 int wf_blocks_per_cu(int precision, int kernel, size_t lds);

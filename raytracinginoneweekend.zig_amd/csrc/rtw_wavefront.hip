@@ -166,6 +166,93 @@ __device__ __forceinline__ bool group_has_work(const WfArgs<R>& A) {
   return __syncthreads_or(work) != 0;
 }
 
+// One shading step of a lane's path (`valid`): background on a miss
+// (main.zig:109-112) or Material.scatter (material.zig:22-121); a finished
+// sample adds to its slot's f64 chunk sum, a finished chunk publishes it and
+// the slot takes the next unit from the segment's reservoir; the slot's next
+// sample starts at once.  Wave-converged (coop_reject, take_unit).  Returns
+// whether the lane holds a live path afterwards.  STATS: count finished
+// samples and shaded segments (rtw_render_counts); FIN: also as the
+// in-register drain's own counts (stats 9, 10: rtw_render_counts_ex).
+template <typename R, bool F32, bool STATS, bool FIN = false>
+__device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R>& T, uint32_t lid, bool valid,
+                                           Lane<R>& L, uint32_t slot, int hit, R tmax, uint32_t& qnext,
+                                           uint32_t& qend) {
+  const uint32_t npix = A.t.row_count * A.t.W;
+  bool ended = false, shading = false, miss = false;
+  uint32_t kind = 0;
+  if (valid) {
+    if (hit < 0) {  // miss: background (main.zig:109-112)
+      miss = true;
+      ended = true;
+    } else {
+      kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
+      shading = true;
+    }
+  }
+  // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
+  const bool nb = shading && kind <= 2u;
+  R b3[3] = {(R)0, (R)0, (R)0};
+  if (__any(nb)) coop_reject<R, 3, true>(nb, L.rs, b3, T.slots, lid);
+  if (shading) {
+    if (scatter_hit<R, F32>(T, L, hit, tmax, kind, b3))
+      ended = true;  // absorbed: emitted == 0 (material.zig:31-38)
+    else if (L.depth == A.t.max_depth)
+      ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
+  }
+  // A finished sample adds to its slot's chunk sum (main.zig:393).
+  bool need_unit = false, need_sample = false;
+  uint32_t unit = 0, s = 0;
+  if (ended) {
+    unit = A.home_unit[slot];
+    s = A.home_s[slot] + 1u;
+    double* hs = A.home_sum + 3 * (size_t)slot;
+    double sx = hs[0], sy = hs[1], sz = hs[2];
+    if (miss) {
+      const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
+      sx += (double)col.x;
+      sy += (double)col.y;
+      sz += (double)col.z;
+    }
+    uint32_t px, ly, c;
+    decode_unit(A.t, unit, px, ly, c);
+    if (s == chunk_end(A.t, c)) {  // unit done: publish the chunk sum
+      double* dst = A.t.partial + ((size_t)c * npix + (size_t)ly * A.t.W + px) * 3;
+      dst[0] = sx;
+      dst[1] = sy;
+      dst[2] = sz;
+      need_unit = true;
+    } else {
+      if (miss) hs[0] = sx, hs[1] = sy, hs[2] = sz;
+      A.home_s[slot] = s;
+      need_sample = true;
+    }
+  }
+  if (take_unit(A.t, need_unit, lid, qnext, qend, unit)) {
+    uint32_t px, ly, c;
+    decode_unit(A.t, unit, px, ly, c);
+    s = c * A.t.chunk;
+    A.home_unit[slot] = unit;
+    A.home_s[slot] = s;
+    double* hs = A.home_sum + 3 * (size_t)slot;
+    hs[0] = hs[1] = hs[2] = 0.0;
+    need_sample = true;
+  }
+  if (need_sample) start_path(A.t, unit, s, L);
+  if constexpr (STATS) {
+    const uint32_t ns = (uint32_t)__popcll(__ballot(ended)), nv = (uint32_t)__popcll(__ballot(valid));
+    if (lid == 0) {
+      atomicAdd(A.t.stats + 0, (unsigned long long)ns);
+      atomicAdd(A.t.stats + 1, (unsigned long long)nv);
+      if (FIN) {
+        atomicAdd(A.t.stats + 9, (unsigned long long)nv);
+        atomicAdd(A.t.stats + 10, (unsigned long long)ns);
+      }
+    }
+  }
+  return valid && (!ended || need_sample);
+}
+
 // ---------------------------------------------------------------- generate --
 // Every slot of the wave's segments takes a unit and starts its first sample.
 template <typename R, bool F32>
@@ -262,7 +349,6 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
     continue;
   }
   const uint32_t base = seg * kSegCap;
-  const uint32_t npix = A.t.row_count * A.t.W;
   uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
   for (uint32_t k = 0; k < n_in; k += 64) {  // wave-uniform: coop_reject runs converged
     const uint32_t i = base + k + lid;
@@ -277,80 +363,57 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
       hit = A.hit_k[i];
       tmax = A.hit_t[i];
     }
-    bool ended = false, shading = false, miss = false;
-    uint32_t kind = 0;
-    if (valid) {
-      if (hit < 0) {  // miss: background (main.zig:109-112)
-        miss = true;
-        ended = true;
-      } else {
-        kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
-        shading = true;
-      }
-    }
-    // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
-    const bool nb = shading && kind <= 2u;
-    R b3[3] = {(R)0, (R)0, (R)0};
-    if (__any(nb)) coop_reject<R, 3, true>(nb, L.rs, b3, T.slots, lid);
-    if (shading) {
-      if (scatter_hit<R, F32>(T, L, hit, tmax, kind, b3))
-        ended = true;  // absorbed: emitted == 0 (material.zig:31-38)
-      else if (L.depth == A.t.max_depth)
-        ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
-    }
-    // A finished sample adds to its slot's chunk sum (main.zig:393).
-    bool need_unit = false, need_sample = false;
-    uint32_t unit = 0, s = 0;
-    if (ended) {
-      unit = A.home_unit[slot];
-      s = A.home_s[slot] + 1u;
-      double* hs = A.home_sum + 3 * (size_t)slot;
-      double sx = hs[0], sy = hs[1], sz = hs[2];
-      if (miss) {
-        const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
-        sx += (double)col.x;
-        sy += (double)col.y;
-        sz += (double)col.z;
-      }
-      uint32_t px, ly, c;
-      decode_unit(A.t, unit, px, ly, c);
-      if (s == chunk_end(A.t, c)) {  // unit done: publish the chunk sum
-        double* dst = A.t.partial + ((size_t)c * npix + (size_t)ly * A.t.W + px) * 3;
-        dst[0] = sx;
-        dst[1] = sy;
-        dst[2] = sz;
-        need_unit = true;
-      } else {
-        if (miss) hs[0] = sx, hs[1] = sy, hs[2] = sz;
-        A.home_s[slot] = s;
-        need_sample = true;
-      }
-    }
-    if (take_unit(A.t, need_unit, lid, qnext, qend, unit)) {
-      uint32_t px, ly, c;
-      decode_unit(A.t, unit, px, ly, c);
-      s = c * A.t.chunk;
-      A.home_unit[slot] = unit;
-      A.home_s[slot] = s;
-      double* hs = A.home_sum + 3 * (size_t)slot;
-      hs[0] = hs[1] = hs[2] = 0.0;
-      need_sample = true;
-    }
-    if (need_sample) start_path(A.t, unit, s, L);
-    push_path(A.out, base, out_n, valid && (!ended || need_sample), L, slot);
-    if constexpr (STATS) {
-      const uint32_t ns = (uint32_t)__popcll(__ballot(ended)), nv = (uint32_t)__popcll(__ballot(valid));
-      if (lid == 0) {
-        atomicAdd(A.t.stats + 0, (unsigned long long)ns);
-        atomicAdd(A.t.stats + 1, (unsigned long long)nv);
-      }
-    }
+    const bool live = shade_step<R, F32, STATS>(A, T, lid, valid, L, slot, hit, tmax, qnext, qend);
+    push_path(A.out, base, out_n, live, L, slot);
   }
   if (lid == 0) {
     A.seg_out[seg] = out_n;
     A.seg_resv[2 * seg] = qnext;
     A.seg_resv[2 * seg + 1] = qend;
   }
+  }
+}
+
+// ------------------------------------------------------------------ finish --
+// The drain in registers: once the unit queue runs dry the queue empties
+// slowly (a slot runs the rest of its unit's samples one after another, and
+// long glass paths finish last), and each (extend, shade) pair would move a
+// sparse queue through HBM for a few paths per segment.  wf_finish runs once,
+// one wave per segment: the wave loads its segment's live paths (queue A,
+// ready for extend) and loops closest hit + shade_step in registers until
+// every lane's slot is done — the same per-sample arithmetic and chunk-sum
+// order, so the same bits; slots still take units from the segment's
+// reservoir and the device queue, so the kernel is correct whenever it runs.
+template <typename R, bool F32, bool STATS>
+__global__ void __launch_bounds__(kTraceBlock) wf_finish(WfArgs<R> A) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const uint32_t lid = lane_id();
+  if (!group_has_work(A)) return;
+  const SceneView<R> S = A.t.sc;
+  const LdsTables<R> T = stage_tables<R>(S, lds_raw);
+  const R tmin = A.t.tmin, pre_k = A.t.pre_k;
+  KStats st;
+  static_assert(kSegCap == 64, "one path per lane per segment");
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+    const uint32_t n_in = A.seg_in[seg];
+    if (n_in == 0u) continue;  // every slot of the segment retired: no unit is left for it
+    uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1];
+    Lane<R> L{};
+    L.skip = -1;
+    uint32_t slot = 0;
+    bool live = lid < n_in;
+    if (live) load_path(A.in, seg * kSegCap + lid, L, slot);
+    while (__any(live)) {  // wave-converged loop; a lane's path advances one segment per pass
+      int hit = -1;
+      R tmax = (R)__builtin_huge_val();
+      if (live) closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+      live = shade_step<R, F32, STATS, true>(A, T, lid, live, L, slot, hit, tmax, qnext, qend);
+    }
+    if (lid == 0) {
+      A.seg_in[seg] = 0u;
+      A.seg_resv[2 * seg] = qnext;
+      A.seg_resv[2 * seg + 1] = qend;
+    }
   }
 }
 
@@ -382,8 +445,12 @@ static hipError_t launch3(int k, const WfArgs<R>& a, uint32_t grid, size_t lds, 
     hipLaunchKernelGGL((wf_extend<R, F32>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (k == 2)
     hipLaunchKernelGGL((wf_shade<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
-  else
+  else if (k == 3)
     hipLaunchKernelGGL((wf_shade<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 4)
+    hipLaunchKernelGGL((wf_finish<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else
+    hipLaunchKernelGGL((wf_finish<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
@@ -394,6 +461,12 @@ hipError_t launch_wf_extend_f64(const WfArgs<double>& a, uint32_t g, size_t l, h
 }
 hipError_t launch_wf_shade_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
   return launch3<double, false>(stats ? 3 : 2, a, g, l, s);
+}
+hipError_t launch_wf_finish_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<double, false>(stats ? 5 : 4, a, g, l, s);
+}
+hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<float, true>(stats ? 5 : 4, a, g, l, s);
 }
 hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<float, true>(0, a, g, l, s);

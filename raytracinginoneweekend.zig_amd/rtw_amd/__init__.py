@@ -105,6 +105,8 @@ def lib() -> C.CDLL:
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.rtw_render_counts.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                     C.c_uint64 * 4]
+    L.rtw_render_counts_ex.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
+                                       C.c_uint64 * 6]
     _lib = L
     return L
 
@@ -238,11 +240,11 @@ class DeviceScene:
                                        timer.h if timer is not None else None))
 
     def counts(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int) -> dict:
-        out = (C.c_uint64 * 4)()
-        _check(lib().rtw_render_counts(self.h, C.byref(cam), C.byref(params), C.c_void_p(workspace_ptr),
-                                       workspace_bytes_, out))
+        out = (C.c_uint64 * 6)()
+        _check(lib().rtw_render_counts_ex(self.h, C.byref(cam), C.byref(params), C.c_void_p(workspace_ptr),
+                                          workspace_bytes_, out))
         return {"samples": int(out[0]), "segments": int(out[1]), "static_tests": int(out[2]),
-                "moving_tests": int(out[3])}
+                "moving_tests": int(out[3]), "drain_segments": int(out[4]), "drain_samples": int(out[5])}
 
     def close(self):
         if self.h:

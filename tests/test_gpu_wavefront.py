@@ -1,5 +1,6 @@
 """GPU parity of the wavefront engine (BASELINE.json configs[3]: SoA path
-queues in HBM, per-bounce extend/shade kernels, persistent grids).
+queues in HBM, per-bounce extend/shade kernels, persistent grids, and the
+in-register drain wf_finish once slots retire).
 
 It computes the same Tier-B image as the megakernel: every sample runs the
 same device functions in the same order and a home slot adds its unit's
@@ -15,6 +16,15 @@ from helpers import diff_stats, to_oracle_camera, to_oracle_scene
 from test_gpu_parity import ASPECT, assert_parity, custom_scene, oracle_render
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["finish", "queues"])
+def drain(request, monkeypatch):
+    """Every test runs with both drains: wf_finish in registers once slots
+    retire (the default) and the (extend, shade) queues to the end
+    (RTW_WF_FINISH=0, read by the library on every render)."""
+    monkeypatch.setenv("RTW_WF_FINISH", "1" if request.param == "finish" else "0")
+    return request.param
 
 
 @pytest.fixture(scope="module")
@@ -113,7 +123,7 @@ def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
 
 
 @pytest.mark.parametrize("w,spp,paths", [(400, 128, 360_000), (1200, 64, 0), (160, 40, 64)])
-def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths):
+def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, drain):
     """Statistics pass: the wavefront shades exactly W*H*spp samples and the
     megakernel's number of bounce segments.  Duplicated or lost units would
     leave the image bits unchanged (a unit's samples are deterministic) but
@@ -130,3 +140,9 @@ def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths):
     torch.cuda.synchronize()
     assert mk["samples"] == w * h * spp
     assert (wf["samples"], wf["segments"]) == (mk["samples"], mk["segments"])
+    # the in-register drain's share (rtw_render_counts_ex): part of the same totals
+    assert mk["drain_segments"] == mk["drain_samples"] == 0
+    if drain == "queues":
+        assert wf["drain_segments"] == wf["drain_samples"] == 0
+    else:
+        assert 0 < wf["drain_segments"] < wf["segments"] and 0 < wf["drain_samples"] < wf["samples"]

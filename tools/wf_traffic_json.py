@@ -1,5 +1,5 @@
 """HBM traffic of one wavefront frame (wf_extend + wf_shade, every bounce
-launch of the frame) from the FETCH_SIZE / WRITE_SIZE PMC passes of
+launch of the frame, + wf_finish) from the FETCH_SIZE / WRITE_SIZE PMC passes of
 tools/gpu_pmc_wf.sh -> profiles/<tag>/wf_traffic.json, read by bench.py for
 wavefront_variant.roofline.traffic.  FETCH_SIZE is doubled (gfx950 tallies
 128-B reads at 64 B, MI355X_MICROARCH.md §HBM); units are KB (rocprofv3).
@@ -11,7 +11,7 @@ import sys
 
 fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
 frames = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-KERNELS = ("wf_extend", "wf_shade")
+KERNELS = ("wf_extend", "wf_shade", "wf_finish")
 
 
 def total(d, name):
@@ -36,6 +36,6 @@ res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", 
        "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one 1200x675x500 f64 "
                  "wavefront render (tools/prof_run.py wf64); bytes = 2*FETCH_SIZE + WRITE_SIZE (KB x 1024), "
-                 "summed over every wf_extend and wf_shade launch of the frame"}
+                 "summed over every wf_extend and wf_shade launch of the frame and its wf_finish (in-register drain)"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
