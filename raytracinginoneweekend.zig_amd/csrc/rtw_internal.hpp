@@ -172,7 +172,10 @@ constexpr uint32_t kMaxXfOps = 4;    // ops per transform chain (== RTW_MAX_XFOR
 constexpr uint32_t kNodeWords = 16;  // 32-bit words per BVH node
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder caps the depth)
-constexpr uint32_t kMaxLeafPrims = 4;
+#ifndef RTW_MAX_LEAF_PRIMS
+#define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
+#endif
+constexpr uint32_t kMaxLeafPrims = RTW_MAX_LEAF_PRIMS;
 
 struct WorldView {
   const double* prim;
