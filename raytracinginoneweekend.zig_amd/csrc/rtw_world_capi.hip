@@ -140,7 +140,10 @@ class Builder {
     for (int k = 1; k < 3; ++k)
       if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
     if (sah && cb.hi[axis] > cb.lo[axis]) {
-      constexpr int kBins = 16;
+#ifndef RTW_SAH_BINS
+#define RTW_SAH_BINS 256  // profiles/r01/world_sah_bins_ab.txt
+#endif
+      constexpr int kBins = RTW_SAH_BINS;
       double best = INFINITY;
       int best_axis = -1, best_bin = -1;
       for (int k = 0; k < 3; ++k) {
