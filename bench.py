@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """bench.py — Msamples/s of the RTIOW cover-scene render on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32]
-  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32] [--config 1|2]
+  (N > 1: one rank per GPU, RCCL backend.  Either launched by
+  torch.distributed.run, or — plain `python bench.py --gpus N` — this script
+  starts torch.distributed.run itself as a child process before touching the
+  GPU; rank 0 prints the one JSON line, with "dist": backend, world size,
+  samples per rank and the time of one gather.)
 
 Workload (BASELINE.json configs[1]): cover scene (generateRandomScene,
 DefaultPrng.init(42), main.zig:157-221), 1200x675 (16:9), 500 spp per GPU,
@@ -45,7 +49,7 @@ PEAK_FP32_VALU_TF = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def parse():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -56,12 +60,19 @@ def parse():
     ap.add_argument("--wf-paths", type=int, default=0, help="wavefront in-flight paths (0 = library default)")
     ap.add_argument("--no-wavefront-variant", action="store_true")
     ap.add_argument("--no-world-variants", action="store_true", help="skip the configs[4] globe and Cornell lines")
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2],
+                    help="BASELINE config: 1 = 1200x675, 500 spp per GPU (weak scaling, default); "
+                         "2 = 3840x2160 at 2000 spp for the whole job (strong scaling)")
     ap.add_argument("--spp", type=int, default=SPP, help="spp per GPU (default 500 = configs[1])")
     ap.add_argument("--width", type=int, default=W_IMG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32-variant", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=16, help="spp of the bounded CPU sample")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def parse():
+    return parse_args()
 
 
 def traffic_per_launch(args, W, H, spp):
@@ -264,8 +275,82 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
                     "same Tier-B image as the megakernel, bit for bit"}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, n, port):
+    """The torch.distributed.run command that starts one rank per GPU with the
+    same bench arguments (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(args, argv) -> int | None:
+    """`python bench.py --gpus N` with N > 1 and no rank environment: start N
+    rank processes (one per GPU) as children and return their exit code.
+    Runs before anything touches the GPU (the parent never initialises HIP,
+    and starts the ranks as child processes, never by exec)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = launch_command(argv, args.gpus, free_port())
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args):
+    """RTW_BENCH_DRYRUN=1: the launcher, rendezvous, shard split, gather and
+    max-over-ranks path of a multi-rank run without a GPU (gloo, CPU tensors,
+    no rendering) — the CPU test of the launcher path (tests/test_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+
+    from rtw_amd.shard import gather_image, shard_rows
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    W, H, spp = workload(args, world)
+    rb, rs, rc = shard_rows(H, rank, world)
+    out = torch.full((rc, 4, 3), rank, dtype=torch.uint8)
+    img = gather_image(out, H, rank, world)
+    samples = torch.tensor([float(rc * W * spp)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(samples)
+    if rank == 0:
+        ok = bool((img[:, 0, 0] == torch.arange(H) % world).all())
+        print(json.dumps({"dry_run": True, "dist": {"backend": dist.get_backend() if world > 1 else None,
+                                                    "world_size": world},
+                          "width": W, "height": H, "spp_frame": spp, "samples_all": samples.item(),
+                          "rows_interleaved_ok": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def workload(args, world):
+    """(W, H, frame spp) of the run.  configs[1] (default): 1200x675, 500 spp per
+    GPU (weak scaling: the frame gets N x 500 spp).  configs[2] (--config 2):
+    3840x2160 at 2000 spp for the whole job (strong scaling: total work fixed,
+    rows split over the ranks)."""
+    import rtw_amd as R
+    if args.config == 2:
+        return 3840, R.image_height(3840, ASPECT), 2000
+    return args.width, R.image_height(args.width, ASPECT), args.spp * world
+
+
 def main():
     args = parse()
+    rc = maybe_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if os.environ.get("RTW_BENCH_DRYRUN"):
+        return dry_run(args)
     import torch
     import torch.distributed as dist
 
@@ -292,9 +377,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    W = args.width
-    H = R.image_height(W, ASPECT)
-    spp = args.spp * world  # weak scaling: the frame gets N x spp
+    W, H, spp = workload(args, world)  # configs[1]: the frame gets N x spp (weak); configs[2]: fixed (strong)
     sph, mats, _ = R.cover_scene(SEED)
     cam = R.cover_camera(ASPECT)
     rb, rs, rc = shard_rows(H, rank, world)
@@ -334,13 +417,25 @@ def main():
     for t in timers:
         t.close()
 
+    dist_info = {"backend": None, "world_size": 1, "samples_per_rank": [samples_rank], "gather_ms": None}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([samples_rank], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tot)
-        samples_all = float(tot.item())
+        per_rank = [torch.zeros(1, dtype=torch.float64, device=f"cuda:{local}") for _ in range(world)]
+        dist.all_gather(per_rank, torch.tensor([float(samples_rank)], dtype=torch.float64, device=f"cuda:{local}"))
+        per_rank = [int(x.item()) for x in per_rank]
+        samples_all = float(sum(per_rank))
+        # One more gather, timed alone (it is also inside every timed step above).
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        gather_image(out, H, rank, world)
+        torch.cuda.synchronize()
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "samples_per_rank": per_rank, "gather_ms": round(float(gt.item()) * 1e3, 3)}
     else:
         samples_all = float(samples_rank)
 
@@ -427,14 +522,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == 2 else "weak",
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic: the reference's own scene generator (seed 42); no external data",
-        "config": {"workload": f"RTIOW cover scene {W}x{H}, {args.spp} spp per GPU ({spp} spp frame), depth {DEPTH}, "
-                               f"rows interleaved over {world} GPU(s)",
+        "config": {"workload": (f"BASELINE configs[2]: RTIOW cover scene {W}x{H}, {spp} spp frame, depth {DEPTH}, "
+                                f"rows interleaved over {world} GPU(s)") if args.config == 2 else
+                               (f"BASELINE configs[1]: RTIOW cover scene {W}x{H}, {args.spp} spp per GPU ({spp} spp "
+                                f"frame), depth {DEPTH}, rows interleaved over {world} GPU(s)"),
                    "width": W, "height": H, "spp_frame": spp, "max_depth": DEPTH, "seed": SEED,
                    "precision": args.precision, "parallelism": f"rows{world}"},
+        "dist": dist_info,
         "roofline": roofline,
     }
     res.update(extra)

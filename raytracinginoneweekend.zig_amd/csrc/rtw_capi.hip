@@ -77,20 +77,14 @@ int wf_bpc(int dev, int prec, int kernel, size_t lds) {
   if (e.second == 0 || e.first != lds) e = {lds, rtwk::wf_blocks_per_cu(prec, kernel, lds)};
   return e.second;
 }
-// Kernel tuning variant (rtw_trace.hip VAR bits).  Defaults from the in-process
-// A/B on MI355X (profiles/r01/ab_defaults.txt): both use scalar
-// sphere records, coop_reject for the unit-ball point, the narrow-sphere
-// pretest, scene fields re-read from the kernel argument (512) and the
-// precomputed Schlick r0^2 (kVarR0Table), the rotated loop with one mixed
-// lens-disk / unit-ball cooperative pass (kVarMergedStart) that also makes the
-// time and dielectric draws (kVarPreDraw); f64 at 4 waves/SIMD (128 VGPRs)
-// with the exact fast sqrt (kVarFastSqrt), f32 at 5 waves/SIMD (96 VGPRs).
-// RTW_VARIANT overrides (development knob).
+// Kernel tuning variant (rtw_trace.hip VAR bits): the product library holds
+// one per precision (rtw_internal.hpp kDefaultVarF64 / kDefaultVarF32).
+// RTW_VARIANT selects another one of a -DRTW_MEASURE build (tools/); a value
+// that was not compiled in is refused by launch_all.
 int kernel_variant(uint32_t precision) {
   const char* v = getenv("RTW_VARIANT");
   if (v && *v) return atoi(v);
-  return precision == RTW_PRECISION_F32 ? 8 + 512 + 131072 + 262144 + 524288
-                                         : 4 + 512 + 32768 + 131072 + 262144 + 524288;
+  return precision == RTW_PRECISION_F32 ? rtwk::kDefaultVarF32 : rtwk::kDefaultVarF64;
 }
 
 }  // namespace
@@ -653,6 +647,8 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   const size_t lds = lds_bytes(sc, (int)p->precision);
   if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int var = kernel_variant(p->precision);
+  if (p->engine != RTW_ENGINE_WAVEFRONT && !rtwk::trace_variant_built((int)p->precision, var))
+    return fail(RTW_EINVAL, "RTW_VARIANT=%d: trace kernel variant not built into this library", var);
   const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);
   const int cus = device_cus(dev);
   uint32_t total_units = 0;
@@ -757,6 +753,9 @@ int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* 
   // RTW_PHASE_PROFILE=1: diagnostic build with per-phase s_memtime stamps.
   const char* prof = getenv("RTW_PHASE_PROFILE");
   const int mode = (prof && prof[0] == '1') ? 2 : 1;
+#ifndef RTW_MEASURE
+  if (mode == 2) return fail(RTW_UNSUPPORTED, "RTW_PHASE_PROFILE needs the -DRTW_MEASURE build (tools/gpu_phase.sh)");
+#endif
   const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, mode);
   if (r != RTW_OK) return r;
   HIP_TRY(hipDeviceSynchronize());

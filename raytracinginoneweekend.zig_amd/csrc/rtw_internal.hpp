@@ -86,8 +86,18 @@ struct FinalizeArgs {
 hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int var);
 hipError_t launch_trace_f32(const TraceArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int var);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
-// Resident workgroups per CU for the trace kernel (occupancy query).
+// Resident workgroups per CU for the trace kernel (occupancy query); 0 when
+// `var` is not compiled into this library.
 int trace_blocks_per_cu(int precision, size_t lds, int var);
+// The trace_kernel variant of each precision in the product library (VAR bits
+// of rtw_device.hpp / rtw_trace.hip, chosen by the in-process A/B on MI355X,
+// profiles/r01/ab_defaults.txt): scalar sphere records + 512 (scene fields from
+// the kernel argument) + kVarR0Table + kVarMergedStart + kVarPreDraw; f64 also
+// 4 waves/SIMD (4) + kVarFastSqrt, f32 5 waves/SIMD (8).  Every other variant
+// exists only in the -DRTW_MEASURE build.
+constexpr int kDefaultVarF64 = 4 + 512 + 32768 + 131072 + 262144 + 524288;  // 950788
+constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
+bool trace_variant_built(int precision, int var);
 constexpr int kTraceBlock = 256;
 // Per-wave LDS slots of coop_reject (rtw_trace.hip CoopSlots: 64 x u64 + 64 x u32).
 constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;

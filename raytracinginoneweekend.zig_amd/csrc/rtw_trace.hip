@@ -363,64 +363,61 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinalizeArgs F) {
 
 template <typename R, bool F32, int VAR>
 static void launch_var(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
-#ifndef RTW_ISA_QUICK  // (register-pressure experiments: product variants only)
   if (mode == 1)
     hipLaunchKernelGGL((trace_kernel<R, F32, 1, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+#ifdef RTW_MEASURE  // per-phase s_memtime stamps (diagnostic)
   else if (mode == 2)
     hipLaunchKernelGGL((trace_kernel<R, F32, 2, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
-  else
 #endif
+  else
     hipLaunchKernelGGL((trace_kernel<R, F32, 0, VAR>), dim3(grid), dim3(kTraceBlock), lds, s, a);
 }
+
+// The product library holds ONE variant per precision (kDefaultVarF64 /
+// kDefaultVarF32, rtw_internal.hpp).  The A/B variants of round 1
+// (profiles/r01/ab_*.txt) are compiled only into the measurement build
+// (-DRTW_MEASURE, tools/); any other value is refused (trace_variant_built).
+#ifdef RTW_MEASURE
+#define RTW_AB_VARIANTS(X)                                                                                     \
+  X(0) X(1) X(5) X(9) X(16) X(24) X(32) X(36) X(20) X(68) X(72) X(40) X(4) X(8) X(516) X(1540) X(520) X(1544)  \
+  X(33284) X(66052) X(131588) X(229892) X(197128) X(164356) X(131592) X(426500) X(393736) X(1999364)         \
+  X(1966600) X(950792) X(1016324) X(2064900) X(918020) X(2564) X(4612) X(8708) X(16900)
+#endif
+
+template <bool F32>
+constexpr int default_var() {
+  return F32 ? kDefaultVarF32 : kDefaultVarF64;
+}
+
+bool trace_variant_built(int precision, int var) {
+  if (var == (precision == 1 ? kDefaultVarF32 : kDefaultVarF64)) return true;
+#ifdef RTW_MEASURE
+  switch (var) {
+#define RTW_CASE(v) case v:
+    RTW_AB_VARIANTS(RTW_CASE)
+#undef RTW_CASE
+    return true;
+  }
+#endif
+  return false;
+}
+
 template <typename R, bool F32>
 static hipError_t launch_trace(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
                                int var) {
-  switch (var) {
-#ifndef RTW_ISA_QUICK
-    case 1: launch_var<R, F32, 1>(a, grid, lds, s, mode); break;
-    case 5: launch_var<R, F32, 5>(a, grid, lds, s, mode); break;
-    case 9: launch_var<R, F32, 9>(a, grid, lds, s, mode); break;
-    case 16: launch_var<R, F32, 16>(a, grid, lds, s, mode); break;
-    case 24: launch_var<R, F32, 24>(a, grid, lds, s, mode); break;
-    case 32: launch_var<R, F32, 32>(a, grid, lds, s, mode); break;
-    case 36: launch_var<R, F32, 36>(a, grid, lds, s, mode); break;
-    case 20: launch_var<R, F32, 20>(a, grid, lds, s, mode); break;
-    case 68: launch_var<R, F32, 68>(a, grid, lds, s, mode); break;
-    case 72: launch_var<R, F32, 72>(a, grid, lds, s, mode); break;
-    case 40: launch_var<R, F32, 40>(a, grid, lds, s, mode); break;
-#endif
-    case 4: launch_var<R, F32, 4>(a, grid, lds, s, mode); break;
-    case 8: launch_var<R, F32, 8>(a, grid, lds, s, mode); break;
-    case 516: launch_var<R, F32, 516>(a, grid, lds, s, mode); break;
-    case 1540: launch_var<R, F32, 1540>(a, grid, lds, s, mode); break;
-    case 520: launch_var<R, F32, 520>(a, grid, lds, s, mode); break;
-    case 1544: launch_var<R, F32, 1544>(a, grid, lds, s, mode); break;
-    case 33284: launch_var<R, F32, 33284>(a, grid, lds, s, mode); break;
-    case 66052: launch_var<R, F32, 66052>(a, grid, lds, s, mode); break;
-    case 131588: launch_var<R, F32, 131588>(a, grid, lds, s, mode); break;
-    case 229892: launch_var<R, F32, 229892>(a, grid, lds, s, mode); break;
-    case 197128: launch_var<R, F32, 197128>(a, grid, lds, s, mode); break;
-    case 164356: launch_var<R, F32, 164356>(a, grid, lds, s, mode); break;
-    case 131592: launch_var<R, F32, 131592>(a, grid, lds, s, mode); break;
-    case 164356 + 262144: launch_var<R, F32, 164356 + 262144>(a, grid, lds, s, mode); break;
-    case 131592 + 262144: launch_var<R, F32, 131592 + 262144>(a, grid, lds, s, mode); break;
-    case 426500 + 524288: launch_var<R, F32, 426500 + 524288>(a, grid, lds, s, mode); break;
-    case 393736 + 524288: launch_var<R, F32, 393736 + 524288>(a, grid, lds, s, mode); break;
-    case 950788 + 1048576: launch_var<R, F32, 950788 + 1048576>(a, grid, lds, s, mode); break;
-    case 918024 + 1048576: launch_var<R, F32, 918024 + 1048576>(a, grid, lds, s, mode); break;
-    case 950792: launch_var<R, F32, 950792>(a, grid, lds, s, mode); break;
-    case 950788 + 65536: launch_var<R, F32, 950788 + 65536>(a, grid, lds, s, mode); break;
-    case 950788 + 65536 + 1048576: launch_var<R, F32, 950788 + 65536 + 1048576>(a, grid, lds, s, mode); break;
-    case 918020: launch_var<R, F32, 918020>(a, grid, lds, s, mode); break;
-#ifdef RTW_MEASURE  // phase-duplication measurement builds (tools/)
-    case 516 + 2048: launch_var<R, F32, 516 + 2048>(a, grid, lds, s, mode); break;
-    case 516 + 4096: launch_var<R, F32, 516 + 4096>(a, grid, lds, s, mode); break;
-    case 516 + 8192: launch_var<R, F32, 516 + 8192>(a, grid, lds, s, mode); break;
-    case 516 + 16384: launch_var<R, F32, 516 + 16384>(a, grid, lds, s, mode); break;
-#endif
-    default: launch_var<R, F32, 0>(a, grid, lds, s, mode); break;
+  if (var == default_var<F32>()) {
+    launch_var<R, F32, default_var<F32>()>(a, grid, lds, s, mode);
+    return hipGetLastError();
   }
-  return hipGetLastError();
+#ifdef RTW_MEASURE
+  switch (var) {
+#define RTW_CASE(v) \
+  case v: launch_var<R, F32, v>(a, grid, lds, s, mode); return hipGetLastError();
+    RTW_AB_VARIANTS(RTW_CASE)
+#undef RTW_CASE
+  }
+#endif
+  return hipErrorInvalidValue;  // not built (rtw_capi.hip checks trace_variant_built first)
 }
 
 hipError_t launch_trace_f64(const TraceArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, int mode,
@@ -444,20 +441,20 @@ static int occ(size_t lds) {
     nb = 0;
   return nb;
 }
+// Resident workgroups per CU of a built variant; 0 for a variant not built.
 int trace_blocks_per_cu(int precision, size_t lds, int var) {
+  if (!trace_variant_built(precision, var)) return 0;
   int nb = 0;
-  switch (var) {
-#define RTW_OCC_CASE(v) \
-  case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
-#ifndef RTW_ISA_QUICK
-    RTW_OCC_CASE(1) RTW_OCC_CASE(5) RTW_OCC_CASE(9) RTW_OCC_CASE(16) RTW_OCC_CASE(24) RTW_OCC_CASE(32) RTW_OCC_CASE(36) RTW_OCC_CASE(20) RTW_OCC_CASE(68) RTW_OCC_CASE(72) RTW_OCC_CASE(40)
-#endif
-    RTW_OCC_CASE(0) RTW_OCC_CASE(4) RTW_OCC_CASE(8) RTW_OCC_CASE(516) RTW_OCC_CASE(1540) RTW_OCC_CASE(520) RTW_OCC_CASE(1544) RTW_OCC_CASE(33284) RTW_OCC_CASE(66052) RTW_OCC_CASE(131588) RTW_OCC_CASE(229892) RTW_OCC_CASE(197128) RTW_OCC_CASE(164356) RTW_OCC_CASE(131592) RTW_OCC_CASE(426500) RTW_OCC_CASE(393736) RTW_OCC_CASE(950788) RTW_OCC_CASE(918024) RTW_OCC_CASE(1999364) RTW_OCC_CASE(1966600) RTW_OCC_CASE(950792) RTW_OCC_CASE(918020) RTW_OCC_CASE(1016324) RTW_OCC_CASE(2064900)
+  if (precision == 1 && var == kDefaultVarF32) nb = occ<float, true, kDefaultVarF32>(lds);
+  else if (precision != 1 && var == kDefaultVarF64) nb = occ<double, false, kDefaultVarF64>(lds);
 #ifdef RTW_MEASURE
-    RTW_OCC_CASE(2564) RTW_OCC_CASE(4612) RTW_OCC_CASE(8708) RTW_OCC_CASE(16900)
-#endif
-#undef RTW_OCC_CASE
+  else switch (var) {
+#define RTW_CASE(v) \
+  case v: nb = precision == 1 ? occ<float, true, v>(lds) : occ<double, false, v>(lds); break;
+    RTW_AB_VARIANTS(RTW_CASE)
+#undef RTW_CASE
   }
+#endif
   return nb > 0 ? nb : 1;
 }
 
