@@ -140,6 +140,8 @@ def cpu_baseline(width, height, spp_sample):
     except Exception:
         cpu = "unknown"
     res = {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "kind_detail": "C restatement of the reference's loop (oracle Tier A; Zig is unbuildable here), "
+                          f"timed on {spp_sample} of {SPP} spp and reported as a per-sample rate",
            "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
                      f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
     # Beside it: the GPU's own contract (Tier B, counter RNG, pixels independent)
@@ -158,12 +160,12 @@ def world_variant(R, torch, scene, steps, warmup):
     """A general-world scene on the world kernel (csrc/rtw_world.hip) at the
     scene's own main.zig settings: scene 6 (Cornell box, the reference's
     default scene, 600x600x200) or 7 (BASELINE configs[4]: globe + 10k
-    spheres, BVH, 1200x675x100; synthetic stand-in for the globe texture).
+    spheres, BVH, 1200x675x100, textured with the reference asset sekaichizu.png).
     Timed with HIP events around the world kernel; a counts pass gives the
     BVH statistics (node visits and primitive tests per segment, counted per
     active lane of the wave-cooperative traversal)."""
     from rtw_amd import world as Wd
-    earth = Wd.synthetic_world_map()
+    earth = Wd.earth_map()  # the reference asset assets/sekaichizu.png (configs[4])
     b = Wd.BuiltScene(scene, SEED, image=earth if scene in (4, 7) else None)
     s = b.settings
     cam = b.camera()

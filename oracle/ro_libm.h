@@ -15,7 +15,9 @@
  * floor(u * width) flips with one ulp of atan2), so Tier B DEFINES them as
  * this algorithm; the product (raytracinginoneweekend.zig_amd/csrc/
  * rtw_libm.hpp) implements the same algorithm independently.  Each function
- * is within 1 ulp of glibc (tests/test_libm.py); |x| >= 2^20*pi/2 for sin/cos
+ * is within 1 ulp of glibc (tests/test_world_cpu.py::
+ * test_tierb_libm_product_equals_oracle_and_glibc, tests/native/libm_check.cpp);
+ * |x| >= 2^20*pi/2 for sin/cos
  * (never produced by the reference's scenes) falls back to the host libm.
  * Compiled with -ffp-contract=off: one IEEE operation per source operation.
  */

@@ -627,6 +627,17 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       break;
     }
   }
+  // Every unit must have run: the drain (queues or wf_finish) ran outside the
+  // batch guard above, so check its end state on the device before returning.
+  if (st == RTW_OK) {
+    if (rtwk::launch_wf_check_drained(seg_a, a.seg_resv, segs, ta.counter, ta.total_units, a.live, stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(&poll[0], a.live, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipEventRecord(ev[0], stream) != hipSuccess || hipEventSynchronize(ev[0]) != hipSuccess)
+      st = fail(RTW_EHIP, "wavefront drain check failed to run");
+    else if (poll[0] != 0u)
+      st = fail(RTW_EHIP, "wavefront drain left %u segments/reservoirs with work undone", poll[0]);
+  }
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
   return st;

@@ -158,6 +158,10 @@ hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t grid, size_t ld
 int wf_blocks_per_cu(int precision, int kernel, size_t lds);
 // live = sum of seg_in[0..n_segs) (one workgroup).
 hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* live, hipStream_t s);
+// *bad = violations of the drained state (non-empty segment, unit left in a
+// reservoir, queue head below total_units); 0 after a complete frame.
+hipError_t launch_wf_check_drained(const uint32_t* seg_in, const uint32_t* resv, uint32_t n_segs, const uint32_t* head,
+                                   uint32_t total_units, uint32_t* bad, hipStream_t s);
 
 // ---------------------------------------------------------- world engine --
 // rtw_world.hip / rtw_world_capi.hip: the general-world kernel (all scenes

@@ -8,8 +8,9 @@
 // ulp of atan2 moves a texel index floor(u * width), one ulp of sin moves a
 // noise colour.  The world kernel and the Tier-B oracle (oracle/ro_libm.h,
 // an independent C restatement of the same algorithms) therefore share this
-// definition; tests/test_libm.py checks host builds of both against each
-// other bit for bit and against glibc (<= 1 ulp).  Compiled with
+// definition; tests/test_world_cpu.py::test_tierb_libm_product_equals_oracle_and_glibc
+// (driving tests/native/libm_check.cpp) checks host builds of both against
+// each other bit for bit and against glibc (<= 1 ulp).  Compiled with
 // -ffp-contract=off: one IEEE operation per source operation.  sin/cos with
 // |x| >= 2^20 * pi/2 (the Payne-Hanek range, never produced by the
 // reference's scenes) return the platform libm's value.

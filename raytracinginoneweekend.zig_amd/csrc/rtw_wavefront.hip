@@ -431,6 +431,30 @@ __global__ void __launch_bounds__(1024) wf_count(const uint32_t* seg, uint32_t n
     *live = t;
   }
 }
+// End-of-frame check (after the last bounce batch or wf_finish): every
+// segment's queue is empty, no reservoir still holds a unit below
+// total_units, and the device queue head passed total_units.  Writes the
+// number of violations to *bad (the host reads it; 0 = every unit ran).
+__global__ void __launch_bounds__(1024) wf_check_drained(const uint32_t* seg, const uint32_t* resv, uint32_t n,
+                                                          const uint32_t* head, uint32_t total_units, uint32_t* bad) {
+  __shared__ uint32_t part[16];
+  uint32_t s = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += 1024)
+    s += (seg[i] != 0u) + (resv[2 * i] < min(resv[2 * i + 1], total_units));
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = *head < total_units;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    *bad = t;
+  }
+}
+hipError_t launch_wf_check_drained(const uint32_t* seg, const uint32_t* resv, uint32_t n, const uint32_t* head,
+                                   uint32_t total_units, uint32_t* bad, hipStream_t s) {
+  hipLaunchKernelGGL(wf_check_drained, dim3(1), dim3(1024), 0, s, seg, resv, n, head, total_units, bad);
+  return hipGetLastError();
+}
 hipError_t launch_wf_count(const uint32_t* seg, uint32_t n, uint32_t* live, hipStream_t s) {
   hipLaunchKernelGGL(wf_count, dim3(1), dim3(1024), 0, s, seg, n, live);
   return hipGetLastError();

@@ -276,6 +276,13 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
       delete w;
       return rtw_fail(RTW_EINVAL, "prim %u: kind %u / material %u / xform %d out of range", i, p.kind, p.mat, p.xform);
     }
+    // MovingSphere.center divides by time1 - time0 (hittable.zig:219-221): an
+    // empty or reversed shutter gives a NaN centre, whose box no BVH node
+    // could hold (the BVH would prune what the linear list tests).
+    if (p.kind == RTW_PRIM_MOVING_SPHERE && !(p.a[8] > p.a[7])) {
+      delete w;
+      return rtw_fail(RTW_EINVAL, "prim %u: moving sphere needs time1 > time0 (got %g, %g)", i, p.a[7], p.a[8]);
+    }
     boxes[i] = prim_box(p, p.xform >= 0 ? &d->xforms[p.xform] : nullptr);
     w->bounds.grow(boxes[i]);
     w->has_moving |= p.kind == RTW_PRIM_MOVING_SPHERE;

@@ -13,6 +13,7 @@ Reference correspondence:
 from __future__ import annotations
 
 import ctypes as C
+import os
 import struct
 import zlib
 
@@ -167,12 +168,23 @@ def load_png(path: str) -> np.ndarray:
     return rgba
 
 
+EARTH_PNG = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                         "assets", "sekaichizu.png")
+
+
+def earth_map(path: str = EARTH_PNG) -> np.ndarray:
+    """The reference's globe texture (assets/sekaichizu.png, 500 x 282 RGBA8,
+    ocean = alpha 0; loaded by ImageTexture.init, texture.zig:107-119, for
+    main.zig:226 and BASELINE configs[4]).  The repo carries the reference's
+    asset file unchanged, with its licence note (assets/LICENSE), so the GPU
+    box renders the real texture; decoded by the library's PNG reader."""
+    return load_png(path)
+
+
 def synthetic_world_map(width: int = 500, height: int = 282) -> np.ndarray:
-    """A deterministic stand-in for assets/sekaichizu.png (500 x 282 RGBA8,
-    ocean = alpha 0): smooth 'continents' from a few sinusoids.  The reference
-    asset is not redistributed (third-party licence) and /root/reference does
-    not exist on the GPU box; configs[4] is benchmarked on this map of the
-    same size and format (the texel-fetch pattern is the same)."""
+    """A deterministic map of the globe asset's size and format (500 x 282
+    RGBA8, ocean = alpha 0): smooth 'continents' from a few sinusoids.  Used
+    only by tests that want a texture independent of the asset file."""
     y, x = np.mgrid[0:height, 0:width].astype(np.float64)
     u, v = x / width * 2 * np.pi, y / height * np.pi
     f = np.sin(3 * u) * np.sin(2 * v) + 0.6 * np.sin(5 * u + 1.3) * np.cos(3 * v) + 0.4 * np.cos(7 * u - 2 * v)
@@ -291,4 +303,4 @@ class DeviceWorld:
             pass
 
 
-__all__ = ["BuiltScene", "DeviceWorld", "render_world", "load_png", "synthetic_world_map", "RtwError", "SCENES"]
+__all__ = ["BuiltScene", "DeviceWorld", "render_world", "load_png", "earth_map", "synthetic_world_map", "RtwError", "SCENES"]

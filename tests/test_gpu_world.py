@@ -21,7 +21,7 @@ def W():
 
 @pytest.fixture(scope="module")
 def earth(W):
-    return W.synthetic_world_map()
+    return W.earth_map()  # the reference's assets/sekaichizu.png
 
 
 def built(W, scene, earth):

@@ -27,7 +27,7 @@ def W():
 
 @pytest.fixture(scope="module")
 def earth(W):
-    return W.synthetic_world_map()
+    return W.earth_map()
 
 
 def resolved(t):
@@ -163,12 +163,16 @@ def test_perlin_noise_matches_python_restatement(oracle):
     assert t == abs(ref)
 
 
-@pytest.mark.skipif(not os.path.exists(REF_PNG), reason="reference asset not present (GPU box)")
 def test_load_png_reference_asset(W):
-    img = W.load_png(REF_PNG)
+    img = W.earth_map()
     assert img.shape == (282, 500, 4) and img.dtype == np.uint8
     a = img[..., 3]
     assert (a == 0).any() and (a == 255).any()  # ocean (alpha 0) and land
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PNG), reason="reference tree not present (GPU box)")
+def test_committed_asset_is_the_reference_file(W):
+    assert open(W.EARTH_PNG, "rb").read() == open(REF_PNG, "rb").read()
 
 
 def test_load_png_roundtrip(W, tmp_path):
@@ -227,6 +231,23 @@ def test_world_create_validates_before_the_gpu(W, rtw):
     prims[3].xform = 7
     with pytest.raises(rtw.RtwError):
         W.DeviceWorld(d)
+
+
+def test_world_create_rejects_empty_shutter(W, rtw):
+    """A moving sphere with time1 <= time0 (NaN centre, hittable.zig:219-221)
+    is refused: its box could not bound it, so BVH and linear would differ."""
+    b = W.BuiltScene(1, 42)
+    d = W.WorldDesc()
+    C.memmove(C.byref(d), C.byref(b.desc), C.sizeof(d))
+    prims = (W.Prim * d.n_prims)()
+    C.memmove(prims, d.prims, C.sizeof(prims))
+    k = next(i for i in range(d.n_prims) if prims[i].kind == W.PRIM_MOVING_SPHERE)
+    d.prims = C.cast(prims, C.POINTER(W.Prim))
+    for t0, t1 in ((0.5, 0.5), (1.0, 0.0)):
+        prims[k].a[7], prims[k].a[8] = t0, t1
+        with pytest.raises(rtw.RtwError) as e:
+            W.DeviceWorld(d)
+        assert e.value.status == rtw.RTW_EINVAL and "time1 > time0" in str(e.value)
 
 
 def test_build_scene_rejects(W, rtw):

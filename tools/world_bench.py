@@ -17,7 +17,7 @@ from rtw_amd import world as Wd  # noqa: E402
 
 
 def run(scene, reps=3, spp=None, width=None, linear=False):
-    earth = Wd.synthetic_world_map()
+    earth = Wd.earth_map()
     b = Wd.BuiltScene(scene, 42, image=earth if scene in (4, 7) else None)
     s = b.settings
     W = width or s.width
