@@ -213,8 +213,11 @@ struct WorldArgs {
 };
 
 // occ: register-allocation target (workgroups per CU): 1 (none), 3 or 4.
-hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ);
-int world_blocks_per_cu(size_t lds, int occ);
+// fs: the kernel's feature set, world_feature_set(features of the world):
+// bits 1 noise texture, 2 image texture, 4 transform chains, 8 rects.
+int world_feature_set(uint32_t feat);
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs);
+int world_blocks_per_cu(size_t lds, int occ, int fs);
 constexpr int kWorldBlock = 256;
 size_t world_lds_bytes(uint32_t n_perlins);
 

@@ -31,6 +31,13 @@ namespace rtwk {
 using D = double;
 using V = V3<D>;
 
+// FEAT: the features a world uses (rtw_world_capi.hip world_features); each
+// kernel instantiation compiles only the paths of its features, so a world
+// of plain spheres does not carry the register budget of Perlin noise,
+// transform chains or rects (the budget sets the spills at 4 waves/SIMD).
+constexpr int kFeatNoise = 1, kFeatImage = 2, kFeatXform = 4, kFeatRect = 8;
+constexpr int kFeatAll = kFeatNoise | kFeatImage | kFeatXform | kFeatRect;
+
 __device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
 
 // Translate / RotateY chains (hittable.zig:478-491, :561-600), op 0 outermost.
@@ -128,13 +135,13 @@ __device__ __forceinline__ bool rect_root(const D* r, D ok, D oa, D ob, D dk, D 
 // Returns false when the primitive cannot be hit at t >= tmin; t may be NaN.
 // root_obj: the ray already in the primitive's object space; RCP: use the
 // ray space's a and RN(1/a) (else plain IEEE divisions; same results).
-template <bool RCP>
+template <bool RCP, int FEAT>
 __device__ __forceinline__ bool root_obj(const PrimRec& q, const RaySp& s, D time, D tmin, D& t) {
   const D* r = q.v;
   const V& o = s.o;
   const V& d = s.d;
   const uint32_t kind = q.meta0 & 0xFFu;
-  if (kind <= 1u) {
+  if (!(FEAT & kFeatRect) || kind <= 1u) {
     V c = mk(r[0], r[1], r[2]);
     if (kind == 1u)  // hittable.zig:219-221; r[10] = RN(1 / (time1 - time0))
       c = add(c, mul(mk(r[3], r[4], r[5]), rtwm::div_rn(time - r[7], r[8], r[10])));
@@ -156,12 +163,13 @@ __device__ __forceinline__ bool root_obj(const PrimRec& q, const RaySp& s, D tim
   if (kind == 3u) return rect_root(r, o.y, o.x, o.z, d.y, d.x, d.z, tmin, t);
   return rect_root(r, o.x, o.y, o.z, d.x, d.y, d.z, tmin, t);
 }
+template <int FEAT>
 __device__ __forceinline__ bool prim_root(const WorldView& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
   const int xf = (int)(q.meta0 >> 8) - 1;
-  if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+  if ((FEAT & kFeatXform) && xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
   RaySp s;
   s.o = o, s.d = d;
-  return root_obj<false>(q, s, time, tmin, t);
+  return root_obj<false, FEAT>(q, s, time, tmin, t);
 }
 
 // The adjacent f32 toward +inf / -inf (finite or infinite x; NaN kept).
@@ -190,6 +198,7 @@ __device__ __forceinline__ void accept(WHit& h, D t, int pos, int orig, D tmin) 
 
 // The reference's literal sequential loop (HittableList.hit, :231-244) over
 // the list in its original order; `order` maps list index -> stored position.
+template <int FEAT>
 __device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* order, V o, V d, D time, D tmin,
                                         WHit& h) {
   h.pos = -1;
@@ -198,7 +207,7 @@ __device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* orde
   for (uint32_t i = 0; i < W.n_prims; ++i) {
     const uint32_t k = order[i];
     D t;
-    if (!prim_root(W, load_rec(W.prim + kWorldRec * k), o, d, time, tmin, t)) continue;
+    if (!prim_root<FEAT>(W, load_rec(W.prim + kWorldRec * k), o, d, time, tmin, t)) continue;
     if (h.t < t) continue;  // `t_max < root` rejects; NaN roots are accepted (as in the reference)
     h.t = t;
     h.pos = (int)k;
@@ -206,7 +215,7 @@ __device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* orde
   }
 }
 
-template <int MODE>
+template <int MODE, int FEAT>
 __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack, const V& o, const V& d, D time,
                                         D tmin, WHit& h, unsigned long long& nv, unsigned long long& nt) {
   h.pos = -1;
@@ -221,7 +230,7 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
     for (uint32_t k = 0; k < W.n_prims; ++k) {
       const PrimRec nxt = load_rec(pr + kWorldRec * (k + 1));
       const int xf = (int)(cur.meta0 >> 8) - 1;
-      if (xf != xf_cur) {  // consecutive primitives share a chain (a Box's six rects)
+      if ((FEAT & kFeatXform) && xf != xf_cur) {  // consecutive primitives share a chain (a Box's six rects)
         xf_cur = xf;
         V oo = o, od = d;
         if (xf >= 0) to_object(cptr(W.xform) + kWorldRec * xf, oo, od);
@@ -229,7 +238,7 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
       }
       D t;
       if (MODE == 1) ++nt;
-      if (root_obj<true>(cur, s, time, tmin, t)) accept(h, t, (int)k, (int)cur.orig, tmin);
+      if (root_obj<true, FEAT>(cur, s, time, tmin, t)) accept(h, t, (int)k, (int)cur.orig, tmin);
       cur = nxt;
     }
     return;
@@ -271,13 +280,13 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
       D t;
       if (MODE == 1) ++nt;
       bool ok;
-      if (xf < 0) {  // separate calls: no copies of (o, d) on the untransformed path
-        ok = root_obj<true>(q, ws, time, tmin, t);
+      if (!(FEAT & kFeatXform) || xf < 0) {  // separate calls: no copies of (o, d) on the untransformed path
+        ok = root_obj<true, FEAT>(q, ws, time, tmin, t);
       } else {
         RaySp s;
         s.o = o, s.d = d;
         to_object(cptr(W.xform) + kWorldRec * xf, s.o, s.d);
-        ok = root_obj<false>(q, s, time, tmin, t);
+        ok = root_obj<false, FEAT>(q, s, time, tmin, t);
       }
       if (ok) accept(h, t, (int)k, (int)q.orig, tmin);
     }
@@ -322,13 +331,15 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
 }
 
 // Texture.value (texture.zig:36-144) for the winner's record.
+template <int FEAT>
 __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v, V p) {
   const D* t = W.tex + kWorldRec * ti;
   const uint32_t* th = reinterpret_cast<const uint32_t*>(t);
   switch (th[0]) {
     case 1u:  // checker: only the sign of sin(10x) sin(10y) sin(10z) matters (rtw_math.hpp)
       return rtwm::checker_odd((D)10 * p.x, (D)10 * p.y, (D)10 * p.z) ? ld3(t + 5) : ld3(t + 8);
-    case 2u: {  // noise, texture.zig:101-105 + Perlin.turb/noise (perlin.zig:49-91)
+    case 2u: {  // noise
+      if constexpr (!(FEAT & kFeatNoise)) return mk(0.0, 0.0, 0.0);  // (no noise texture in this world), texture.zig:101-105 + Perlin.turb/noise (perlin.zig:49-91)
       const D* pr = W.perlin + (size_t)th[1] * (256 * 3 + 384);
       const uint32_t* perm = reinterpret_cast<const uint32_t*>(pr + 256 * 3);
       D accum = 0.0, weight = 1.0;
@@ -359,7 +370,8 @@ __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v
       const D kk = 0.5 * (1.0 + rtwl::sin(t[11] * p.z + 10.0 * fabs(accum)));
       return mk(1 * kk, 1 * kk, 1 * kk);
     }
-    case 3u: {  // image, texture.zig:121-144 (row clamp: rtw_world.h)
+    case 3u: {  // image
+      if constexpr (!(FEAT & kFeatImage)) return mk(0.0, 0.0, 0.0);  // (no image texture in this world), texture.zig:121-144 (row clamp: rtw_world.h)
       const uint32_t* im = W.image + 4 * th[2];
       const uint32_t w = im[0], hgt = im[1];
       const D uc = fmax(0.0, fmin(u, 1.0));
@@ -381,7 +393,7 @@ __device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v
 
 // OCC: minimum resident workgroups per CU asked of the register allocator
 // (1 = unconstrained; chosen by A/B on MI355X, rtw_world_capi.hip).
-template <int MODE, int OCC>
+template <int MODE, int OCC, int FEAT>
 __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kBvhStack;  // this wave's stack
@@ -467,8 +479,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       } else {
         if (MODE == 1) ++n_segments;
         WHit h;
-        closest<MODE>(W, margin, stack, L.o, L.d, L.time, tmin, h, n_visits, n_tests);
-        if (__builtin_expect(h.nan, 0)) seq_hit(W, order, L.o, L.d, L.time, tmin, h);
+        closest<MODE, FEAT>(W, margin, stack, L.o, L.d, L.time, tmin, h, n_visits, n_tests);
+        if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, tmin, h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
           rad = add(rad, mulv(L.T, ld3(opaque(kargs<D>())->bg)));
           ended = true;
@@ -479,16 +491,16 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           const uint32_t kind = mt[0] & 0xFFu;
           const int xf = (int)(mt[0] >> 8) - 1;
           V o = L.o, d = L.d;
-          if (xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+          if ((FEAT & kFeatXform) && xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
           V p = add(o, mul(d, h.t)), nrm;
           bool front;
           D tu = 0.0, tv = 0.0;
           const D* mp = W.mat + 8 * mt[1];
           const uint32_t* mh = reinterpret_cast<const uint32_t*>(mp);
           const uint32_t mkind = mh[0], mtex = mh[1];
-          const bool image_tex =
+          const bool image_tex = (FEAT & kFeatImage) &&
               (mkind == 0u || mkind == 3u) && *reinterpret_cast<const uint32_t*>(W.tex + kWorldRec * mtex) == 3u;
-          if (kind <= 1u) {
+          if (!(FEAT & kFeatRect) || kind <= 1u) {
             V c = ld3(r);
             if (kind == 1u) c = add(c, mul(ld3(r + 3), (L.time - r[7]) / r[8]));
             const V outward = divs(sub(p, c), r[6]);
@@ -514,9 +526,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
             front = dot(n0, d) < 0.0;
             nrm = front ? n0 : mul(n0, -1.0);
           }
-          if (xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
+          if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
           if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
-            rad = add(rad, mulv(L.T, tex_value(W, mtex, tu, tv, p)));
+            rad = add(rad, mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p)));
             ended = true;
           } else {
             V ndir, att;
@@ -531,7 +543,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
               }
               ndir = add(nrm, normalized(mk(b3[0], b3[1], b3[2])));
               if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
-              att = tex_value(W, mtex, tu, tv, p);
+              att = tex_value<FEAT>(W, mtex, tu, tv, p);
             } else if (mkind == 1u) {  // Metal (material.zig:59-65)
               const V ud = normalized(L.d);
               const V refl = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
@@ -605,33 +617,56 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 
 size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * (kWorldBlock / 64) * sizeof(uint32_t); }
 
-template <int OCC>
+template <int OCC, int FEAT>
 static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
   if (mode == 1)
-    hipLaunchKernelGGL((world_kernel<1, OCC>), dim3(grid), dim3(kWorldBlock), lds, s, a);
+    hipLaunchKernelGGL((world_kernel<1, OCC, FEAT>), dim3(grid), dim3(kWorldBlock), lds, s, a);
   else
-    hipLaunchKernelGGL((world_kernel<0, OCC>), dim3(grid), dim3(kWorldBlock), lds, s, a);
+    hipLaunchKernelGGL((world_kernel<0, OCC, FEAT>), dim3(grid), dim3(kWorldBlock), lds, s, a);
 }
-hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ) {
+template <int FEAT>
+static void launch_feat(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ) {
   if (occ >= 4)
-    launch_occ<4>(a, grid, lds, s, mode);
+    launch_occ<4, FEAT>(a, grid, lds, s, mode);
   else if (occ == 3)
-    launch_occ<3>(a, grid, lds, s, mode);
+    launch_occ<3, FEAT>(a, grid, lds, s, mode);
   else
-    launch_occ<1>(a, grid, lds, s, mode);
+    launch_occ<1, FEAT>(a, grid, lds, s, mode);
+}
+// Instantiated feature sets: spheres with solid / checker / image textures
+// (scenes 1, 2, 4 and configs[4]'s globe), rects + transforms + lights without
+// noise / image (the Cornell box, scene 5's light), and everything.
+int world_feature_set(uint32_t feat) {
+  if ((feat & ~(uint32_t)kFeatImage) == 0u) return kFeatImage;
+  if ((feat & ~(uint32_t)(kFeatXform | kFeatRect)) == 0u) return kFeatXform | kFeatRect;
+  return kFeatAll;
+}
+hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs) {
+  if (fs == kFeatImage)
+    launch_feat<kFeatImage>(a, grid, lds, s, mode, occ);
+  else if (fs == (kFeatXform | kFeatRect))
+    launch_feat<kFeatXform | kFeatRect>(a, grid, lds, s, mode, occ);
+  else
+    launch_feat<kFeatAll>(a, grid, lds, s, mode, occ);
   return hipGetLastError();
 }
 
-int world_blocks_per_cu(size_t lds, int occ) {
+template <int FEAT>
+static int bpc_feat(size_t lds, int occ) {
   int nb = 0;
   hipError_t e;
   if (occ >= 4)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 4>, kWorldBlock, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 4, FEAT>, kWorldBlock, lds);
   else if (occ == 3)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 3>, kWorldBlock, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 3, FEAT>, kWorldBlock, lds);
   else
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 1>, kWorldBlock, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 1, FEAT>, kWorldBlock, lds);
   return (e == hipSuccess && nb > 0) ? nb : 1;
+}
+int world_blocks_per_cu(size_t lds, int occ, int fs) {
+  if (fs == kFeatImage) return bpc_feat<kFeatImage>(lds, occ);
+  if (fs == (kFeatXform | kFeatRect)) return bpc_feat<kFeatXform | kFeatRect>(lds, occ);
+  return bpc_feat<kFeatAll>(lds, occ);
 }
 
 }  // namespace rtwk

@@ -236,6 +236,7 @@ struct rtw_world_s {
   rtwk::WorldView view{};
   Box bounds;
   bool has_moving = false;
+  uint32_t feat = 0;  // features used (rtw_world.hip kFeat*): picks the kernel instantiation
   uint32_t info[4] = {0, 0, 0, 0};
 };
 
@@ -286,6 +287,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     boxes[i] = prim_box(p, p.xform >= 0 ? &d->xforms[p.xform] : nullptr);
     w->bounds.grow(boxes[i]);
     w->has_moving |= p.kind == RTW_PRIM_MOVING_SPHERE;
+    if (p.xform >= 0) w->feat |= 4u;
+    if (p.kind >= RTW_PRIM_XY_RECT) w->feat |= 8u;
   }
   Bvh bvh;
   // Small worlds (<= kLinearMax primitives: the Cornell box, the Perlin and
@@ -414,6 +417,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.pixels = base + o_pix;
   w->view.node = reinterpret_cast<const float*>(base + o_node);
   w->view.order = reinterpret_cast<const uint32_t*>(base + o_order);
+  for (uint32_t i = 0; i < d->n_textures; ++i)
+    w->feat |= d->textures[i].kind == RTW_TEX_NOISE ? 1u : (d->textures[i].kind == RTW_TEX_IMAGE ? 2u : 0u);
   w->view.n_prims = n;
   for (uint32_t i = 0; i < n; ++i)
     if (d->prims[i].kind <= RTW_PRIM_MOVING_SPHERE) w->view.flags |= rtwk::kWorldHasSpheres;
@@ -499,14 +504,18 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   // Register-allocation target (RTW_WORLD_OCC development knob overrides).
   const char* oc = getenv("RTW_WORLD_OCC");
   const int occ = (oc && *oc) ? atoi(oc) : world_occ_default(w);
-  static int bpc_cache[5] = {0, 0, 0, 0, 0};
+  // Kernel instantiation for the world's features (RTW_WORLD_FEAT=all: the
+  // general kernel, development knob for A/B; every set gives the same bits).
+  const char* fe = getenv("RTW_WORLD_FEAT");
+  const int fs = rtwk::world_feature_set((fe && !std::strcmp(fe, "all")) ? 15u : w->feat);
+  static int bpc_cache[16][5] = {};
   const int oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
-  if (bpc_cache[oi] == 0) bpc_cache[oi] = rtwk::world_blocks_per_cu(lds, oi);
-  const int bpc = bpc_cache[oi];
+  if (bpc_cache[fs][oi] == 0) bpc_cache[fs][oi] = rtwk::world_blocks_per_cu(lds, oi, fs);
+  const int bpc = bpc_cache[fs][oi];
   const uint32_t want = (a.t.total_units + 255) / 256;
   const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
   if (timer && rtw_timer_mark(timer, stream, true) != RTW_OK) return RTW_EHIP;
-  hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode, oi);
+  hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode, oi, fs);
   if (e != hipSuccess) return rtw_fail(RTW_EHIP, "world kernel launch: %s", hipGetErrorString(e));
   if (timer && rtw_timer_mark(timer, stream, false) != RTW_OK) return RTW_EHIP;
   if (d_rgb) return rtw_launch_finalize(p, wsb, d_rgb, d_mean, stream);

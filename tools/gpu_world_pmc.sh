@@ -1,12 +1,19 @@
-# PMC passes over the world kernel (scene $SCENE): issue/wait breakdown, I-cache, instruction mix.
+# PMC passes over the world kernel (scene $SCENE, one render of main.zig's
+# settings; tools/world_prof_run.py): issue / wait breakdown, VALU issue,
+# instruction mix, and the HBM traffic (FETCH_SIZE, WRITE_SIZE in separate
+# passes, per MI355X_MICROARCH.md).  Output: gpurun_out/wpmc_${SCENE}_{a,b,f,w}.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-S=${SCENE:-6}
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wpmc_${S}_a -o run \
-  --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU \
-  -- python tools/world_prof_run.py $S > gpurun_out/wpmc_a.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wpmc_${S}_b -o run \
-  --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA \
-  -- python tools/world_prof_run.py $S > gpurun_out/wpmc_b.log 2>&1
+S=${SCENE:-7}
+run() {  # $1 = pass tag, rest = counters
+  local tag=$1; shift
+  timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wpmc_${S}_$tag -o run \
+    --pmc "$@" -- python tools/world_prof_run.py $S > gpurun_out/wpmc_${S}_$tag.log 2>&1
+}
+run a SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM &&
+run b SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS &&
+run c SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 &&
+run f FETCH_SIZE &&
+run w WRITE_SIZE
