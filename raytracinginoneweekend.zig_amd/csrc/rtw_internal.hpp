@@ -177,7 +177,10 @@ hipError_t launch_wf_check_drained(const uint32_t* seg_in, const uint32_t* resv,
 //   image  : {width, height, byte offset} + one RGBA8 byte pool
 //   node   : 64 B, BVH2 with both child boxes in the parent: f32 lo0.xyz, hi0.xyz,
 //            lo1.xyz, hi1.xyz (each f64 box bound rounded OUTWARD to f32, so a box only
-//            grows), u32 ref0, ref1; ref bit 31 = leaf {first (bits 0-22), count (23-30)}
+//            grows), u32 ref0, ref1; ref bit 31 = leaf {first (bits 0-22), count (23-29),
+//            bit 30 = the leaf's spheres have a packed-f32 pretest record cull[first]}
+//   cull   : 64 B per stored position (used at a leaf's first position): the
+//            megakernel's pair record (rtw_device.hpp PairRec) of the leaf's <= 2 spheres
 //   order  : list index -> stored position (the NaN fallback's sequential loop)
 // Prims are stored in BVH leaf order; `orig` keeps the list index for the
 // reference's tie rule (later object wins).
@@ -185,6 +188,8 @@ constexpr uint32_t kWorldRec = 16;   // doubles per prim / xform / texture recor
 constexpr uint32_t kMaxXfOps = 4;    // ops per transform chain (== RTW_MAX_XFORM_OPS)
 constexpr uint32_t kNodeWords = 16;  // 32-bit words per BVH node
 constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kCullBit = 0x40000000u;  // leaf ref: pretest record present
+constexpr uint32_t kLeafCountMask = 0x7Fu;  // leaf ref: count = (ref >> 23) & mask
 constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder caps the depth)
 #ifndef RTW_MAX_LEAF_PRIMS
 #define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
@@ -201,7 +206,9 @@ struct WorldView {
   const uint8_t* pixels;
   const float* node;
   const uint32_t* order;
+  const float* cull;             // leaf pretest records (kCullBit leaves)
   uint32_t n_prims, n_nodes, n_perlins, flags;
+  float cull_cmax, cull_rho;     // rtw_cull.hpp Cmax and rho_max over the pretested spheres
 };
 constexpr uint32_t kWorldHasSpheres = 1;  // WorldView.flags
 

@@ -271,10 +271,26 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
   const RTW_CONST float* cn = cptr(W.node);
   const RTW_CONST D* pr = cptr(W.prim);
   const RaySp ws = ray_space(o, d, W.flags);
+  // Leaf pretest (kCullBit leaves): the megakernel's packed-f32 bound
+  // (rtw_cull.hpp) for the leaf's <= 2 spheres; x < 0 proves the sphere's
+  // exact discriminant negative for this lane, and a sphere no lane can hit
+  // skips its exact test (the test would reject it in every lane).
+  const float af = (float)ws.a;
+  const rtwc::LaneCull lc = rtwc::lane_cull((float)o.x, (float)o.y, (float)o.z, af, W.cull_cmax);
+  const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, W.cull_rho);
+  const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(W.cull));
   uint32_t sp = 0, node = 0;  // wave-uniform
   auto leaf = [&](uint32_t ref) {
-    const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & 0xFFu;
+    const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & kLeafCountMask;
+    bool need0 = true, need1 = true;
+    if ((FEAT & ~kFeatImage) == 0 && (ref & kCullBit)) {  // sphere worlds (the other sets ignore the bit)
+      const f2 x = cull_pair<1>(ld_pair(ct, first), bc((float)o.x), bc((float)o.y), bc((float)o.z), bc((float)d.x),
+                                bc((float)d.y), bc((float)d.z), bc(lk.na), bc(lk.k), bc((float)time));
+      need0 = __ballot(!lc.ok || !(x.x < 0.0f)) != 0;
+      need1 = __ballot(!lc.ok || !(x.y < 0.0f)) != 0;
+    }
     for (uint32_t k = first; k < first + cnt; ++k) {
+      if (!(k == first ? need0 : (k == first + 1 ? need1 : true))) continue;  // wave-uniform
       const PrimRec q = load_rec(pr + kWorldRec * k);
       const int xf = (int)(q.meta0 >> 8) - 1;
       D t;

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "rtw_hip.h"
+#include "rtw_cull.hpp"
 #include "rtw_internal.hpp"
 
 // rtw_capi.hip helpers shared by both paths (same library).
@@ -189,7 +190,8 @@ class Builder {
   uint32_t child(uint32_t b, uint32_t e, uint32_t depth) {
     // Leaves: few primitives, or the depth cap of the per-lane LDS stack
     // (node() switches to median splits while they still fit the cap).
-    if (e - b <= rtwk::kMaxLeafPrims || (depth >= rtwk::kBvhStack - 1 && e - b <= 255)) return leaf(b, e);
+    if (e - b <= rtwk::kMaxLeafPrims || (depth >= rtwk::kBvhStack - 1 && e - b <= rtwk::kLeafCountMask))
+      return leaf(b, e);
     const uint32_t n = alloc();
     node(n, b, e, depth);
     return n;
@@ -329,6 +331,61 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     const uint32_t meta[4] = {p.kind | ((uint32_t)(p.xform + 1) << 8), p.mat, li, 0u};
     std::memcpy(r + 14, meta, sizeof(meta));
   }
+  // Leaf pretest records (rtw_cull.hpp, the megakernel's packed-f32 bound):
+  // a BVH leaf of <= 2 spheres that are untransformed, narrow (|r| < 100) and
+  // static or moving over the shutter [0, 1] (their f32 time fraction is the
+  // ray's f32 time, as in the cover scene) gets the pair record of its
+  // spheres at cull[first] and kCullBit in its ref; the kernel skips a
+  // sphere's exact test when no lane's pretest survives.
+  std::vector<float> cull;
+  float cull_cmax = 0.0f, cull_rho = 0.0f;
+  if (use_bvh) {
+    auto eligible = [&](uint32_t pos) {
+      const rtw_prim& p = d->prims[bvh.order[pos]];
+      if (p.xform >= 0 || !(std::fabs(p.a[6]) < 100.0)) return false;
+      return p.kind == RTW_PRIM_SPHERE || (p.kind == RTW_PRIM_MOVING_SPHERE && p.a[7] == 0.0 && p.a[8] == 1.0);
+    };
+    std::vector<uint32_t> leaf_refs;  // (node, child) slots whose leaf qualifies
+    double cmax_c = 0.0, cmax_d = 0.0, rho_max = 1.0;
+    for (uint32_t nd = 0; nd < bvh.n_nodes; ++nd) {
+      for (uint32_t c = 0; c < 2; ++c) {
+        uint32_t ref;
+        std::memcpy(&ref, bvh.nodes.data() + (size_t)rtwk::kNodeWords * nd + 12 + c, 4);
+        const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & rtwk::kLeafCountMask;
+        if (!(ref & rtwk::kLeafBit) || cnt == 0 || cnt > 2) continue;
+        bool ok = true;
+        for (uint32_t k = first; k < first + cnt; ++k) ok = ok && eligible(k);
+        if (!ok) continue;
+        leaf_refs.push_back(2 * nd + c);
+        for (uint32_t k = first; k < first + cnt; ++k) {
+          const double* r = prim.data() + (size_t)rtwk::kWorldRec * k;
+          for (int j = 0; j < 3; ++j) cmax_c = std::max(cmax_c, std::fabs(r[j])), cmax_d = std::max(cmax_d, std::fabs(r[3 + j]));
+          rho_max = std::max(rho_max, 2.0 * r[9] + 1.0);
+        }
+      }
+    }
+    cull_cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
+    cull_rho = std::nextafter((float)rho_max, INFINITY);
+    const char* nc = getenv("RTW_WORLD_NOCULL");  // development knob (A/B): no leaf pretest
+    if (!leaf_refs.empty() && cull_cmax <= rtwc::kCmaxLimit && !(nc && *nc)) {
+      cull.assign((size_t)16 * n, 0.0f);
+      for (uint32_t slot : leaf_refs) {
+        float* nw = bvh.nodes.data() + (size_t)rtwk::kNodeWords * (slot / 2) + 12 + (slot & 1);
+        uint32_t ref;
+        std::memcpy(&ref, nw, 4);
+        const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & rtwk::kLeafCountMask;
+        for (uint32_t j = 0; j < cnt; ++j) {  // sphere j of the leaf -> lane j of each f2
+          const double* r = prim.data() + (size_t)rtwk::kWorldRec * (first + j);
+          float* q = cull.data() + (size_t)16 * first + j;
+          for (int k = 0; k < 3; ++k) q[2 * k] = (float)r[k], q[2 * (3 + k)] = -(float)r[3 + k];
+          const float rf = (float)r[6];
+          q[12] = -(rf * rf);
+        }
+        ref |= rtwk::kCullBit;
+        std::memcpy(nw, &ref, 4);
+      }
+    }
+  }
   std::vector<double> xf((size_t)rtwk::kWorldRec * std::max(d->n_xforms, 1u), 0.0);
   for (uint32_t i = 0; i < d->n_xforms; ++i) {
     double* r = xf.data() + (size_t)rtwk::kWorldRec * i;
@@ -379,7 +436,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const size_t o_img = o_perl + al(perl.size() * 8), o_pix = o_img + al(img.size() * 4);
   const size_t o_node = o_pix + al(std::max(pix_bytes, (size_t)4));
   const size_t o_order = o_node + al(std::max(bvh.nodes.size() * 4, (size_t)4));
-  const size_t total = o_order + al((size_t)std::max(n, 1u) * 4);
+  const size_t o_cull = o_order + al((size_t)std::max(n, 1u) * 4);
+  const size_t total = o_cull + al(std::max(cull.size() * 4, (size_t)4));
   std::vector<unsigned char> host(total, 0);
   std::memcpy(host.data() + o_prim, prim.data(), prim.size() * 8);
   std::memcpy(host.data() + o_xf, xf.data(), xf.size() * 8);
@@ -392,6 +450,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
                 (size_t)d->images[i].width * d->images[i].height * 4);
   if (!bvh.nodes.empty()) std::memcpy(host.data() + o_node, bvh.nodes.data(), bvh.nodes.size() * 4);
   if (n) std::memcpy(host.data() + o_order, list_to_pos.data(), (size_t)n * 4);
+  if (!cull.empty()) std::memcpy(host.data() + o_cull, cull.data(), cull.size() * 4);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     delete w;
@@ -417,6 +476,9 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.pixels = base + o_pix;
   w->view.node = reinterpret_cast<const float*>(base + o_node);
   w->view.order = reinterpret_cast<const uint32_t*>(base + o_order);
+  w->view.cull = reinterpret_cast<const float*>(base + o_cull);
+  w->view.cull_cmax = cull_cmax;
+  w->view.cull_rho = cull_rho;
   for (uint32_t i = 0; i < d->n_textures; ++i)
     w->feat |= d->textures[i].kind == RTW_TEX_NOISE ? 1u : (d->textures[i].kind == RTW_TEX_IMAGE ? 2u : 0u);
   w->view.n_prims = n;
