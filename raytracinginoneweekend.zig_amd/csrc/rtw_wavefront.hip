@@ -286,8 +286,19 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
 }
 
 // ------------------------------------------------------------------ extend --
+// The megakernel's closest-hit instantiation: scene fields re-read from the
+// kernel argument inside closest_hit (trace VAR bit 512: the SceneView copy
+// would sit in SGPRs for the whole kernel, at the 100-SGPR limit), the exact
+// fast f64 sqrt (kVarFastSqrt), and a waves-per-SIMD target for the register
+// allocator (kWfExtendOcc, chosen by A/B on MI355X).
+#ifndef RTW_WF_EXT_OCC
+#define RTW_WF_EXT_OCC 6
+#endif
+constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
+template <typename R>
+constexpr int kWfExtendVar = sizeof(R) == 8 ? kVarFastSqrt : 0;
 template <typename R, bool F32>
-__global__ void __launch_bounds__(kTraceBlock) wf_extend(WfArgs<R> A) {
+__global__ void __launch_bounds__(kTraceBlock, kWfExtendOcc) wf_extend(WfArgs<R> A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   if (!group_has_work(A)) return;
   const SceneView<R> S = A.t.sc;
@@ -318,7 +329,11 @@ __global__ void __launch_bounds__(kTraceBlock) wf_extend(WfArgs<R> A) {
     if (cur_ok) {
       int hit = -1;
       R tmax = (R)__builtin_huge_val();
+#ifdef RTW_WF_EXT_LEGACY
       closest_hit<R, F32, 0, 0>(S, T, cur, tmin, pre_k, lid, st, hit, tmax);
+#else
+      closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, cur, tmin, pre_k, lid, st, hit, tmax);
+#endif
       const uint32_t i = seg * kSegCap + lid;
       A.hit_t[i] = tmax;
       A.hit_k[i] = hit;
