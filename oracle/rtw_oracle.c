@@ -325,6 +325,7 @@ typedef struct {
   V3 bg;
   uint64_t *rng;
   ro_stats st;
+  uint32_t flags; /* RO_BOOK1_* (ro_render_tier_a_ex), 0 = the current main.zig */
 } CtxA;
 
 /* MovingSphere.center, hittable.zig:219-221 */
@@ -456,7 +457,14 @@ static int scatter_a(CtxA *cx, const RayA *r_in, const HitA *rec, V3 *att, RayA 
 static V3 ray_color_a(CtxA *cx, const RayA *r, uint32_t depth) {
   if (depth == 0) return v3(0.0, 0.0, 0.0);
   HitA rec;
-  if (!world_hit(cx, r, 0.001, INFINITY, &rec)) return cx->bg;
+  if (!world_hit(cx, r, 0.001, INFINITY, &rec)) {
+    if (cx->flags & RO_BOOK1_SKY) { /* the Book-1 sky of the reference's README image (ro_render_tier_a_ex) */
+      const V3 ud = vnormalized(r->dir);
+      const double t = 0.5 * (ud.y + 1.0);
+      return vadd(vmul(v3(1.0, 1.0, 1.0), 1.0 - t), vmul(v3(0.5, 0.7, 1.0), t));
+    }
+    return cx->bg;
+  }
   RayA scattered;
   V3 att;
   const V3 emitted = v3(0, 0, 0); /* Material.emitted, material.zig:31-38 */
@@ -466,7 +474,7 @@ static V3 ray_color_a(CtxA *cx, const RayA *r, uint32_t depth) {
 }
 
 /* Camera.getRay, main.zig:91-100 */
-static RayA get_ray_a(const ro_camera *cam, uint64_t rng[4], double s, double t, uint64_t *draws) {
+static RayA get_ray_a(const ro_camera *cam, uint64_t rng[4], double s, double t, uint64_t *draws, int time_draw) {
   const V3 rd = vmul(rand_in_unit_disk(rng, draws), cam->lens_radius);
   const V3 offset = vadd(vmul(vload(cam->u), rd.x), vmul(vload(cam->v), rd.y));
   const V3 dir = vsub(vsub(vadd(vadd(vload(cam->lower_left_corner), vmul(vload(cam->horizontal), s)),
@@ -476,6 +484,10 @@ static RayA get_ray_a(const ro_camera *cam, uint64_t rng[4], double s, double t,
   RayA r;
   r.origin = vadd(vload(cam->origin), offset);
   r.dir = dir;
+  if (!time_draw) { /* Book-1 camera: no shutter time */
+    r.time = cam->time0;
+    return r;
+  }
   r.time = rand_range(rng, cam->time0, cam->time1);
   if (draws) *draws += 1;
   return r;
@@ -488,23 +500,30 @@ uint8_t ro_quantize(double c, double scale) {
   return (uint8_t)(256.0 * cl);
 }
 
-/* Render loop, main.zig:378-402: j rows, i columns, s samples, one stream. */
-void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double bg[3],
-                      uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
-                      uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats) {
+/* Render loop, main.zig:378-402: j rows, i columns, s samples, one stream.
+ * ro_render_tier_a_ex: the same loop over the first `rows` values of j only
+ * (the stream of row j depends on rows < j alone), with `flags` selecting the
+ * Book-1 variant of the README image (RO_BOOK1_SKY: the gradient sky of the
+ * book's first volume instead of `bg`; RO_BOOK1_NO_TIME: Camera.getRay draws
+ * no shutter time) — test infrastructure for tests/test_readme_image.py. */
+void ro_render_tier_a_ex(const ro_scene *scene, const ro_camera *cam, const double bg[3],
+                         uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
+                         uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats,
+                         uint32_t flags, uint32_t rows) {
   CtxA cx;
   memset(&cx, 0, sizeof(cx));
   cx.scene = scene;
   cx.bg = vload(bg);
   cx.rng = rng;
-  for (uint32_t j = 0; j < H; ++j) {
+  cx.flags = flags;
+  for (uint32_t j = 0; j < H && j < rows; ++j) {
     for (uint32_t i = 0; i < W; ++i) {
       V3 pc = v3(0.0, 0.0, 0.0);
       for (uint32_t s = 0; s < spp; ++s) {
         const double u = ((double)i + rand01(rng)) / ((double)W - 1.0);
         const double v = ((double)j + rand01(rng)) / ((double)H - 1.0);
         cx.st.draws += 2;
-        const RayA r = get_ray_a(cam, rng, u, v, &cx.st.draws);
+        const RayA r = get_ray_a(cam, rng, u, v, &cx.st.draws, !(flags & RO_BOOK1_NO_TIME));
         pc = vadd(pc, ray_color_a(&cx, &r, depth));
         cx.st.samples++;
       }
@@ -517,6 +536,11 @@ void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double 
     }
   }
   if (stats) *stats = cx.st;
+}
+void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double bg[3],
+                      uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
+                      uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats) {
+  ro_render_tier_a_ex(scene, cam, bg, W, H, spp, depth, rng, rgb, sum_out, stats, 0u, H);
 }
 
 /* main(), main.zig:295-402 with scene == 1 and the given image parameters. */

@@ -110,6 +110,12 @@ uint32_t ro_image_height(uint32_t width, double aspect); /* main.zig:306 */
 /* ---- Tier A: the reference render loop (main.zig:378-402) ----
  * rng: state after the scene build.  rgb: W*H*3, top row first (main.zig:396).
  * sum_out (optional): W*H*3 f64 per-pixel sums, same layout. */
+#define RO_BOOK1_SKY 1u
+#define RO_BOOK1_NO_TIME 2u
+void ro_render_tier_a_ex(const ro_scene *scene, const ro_camera *cam, const double bg[3],
+                         uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
+                         uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats,
+                         uint32_t flags, uint32_t rows);
 void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double bg[3],
                       uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
                       uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats);

@@ -9,6 +9,7 @@ KATs and the independent Python restatement in rtw_oracle_py.py).
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import subprocess
 
@@ -101,6 +102,9 @@ def lib():
                                     C.c_void_p, C.POINTER(Stats)]
         L.ro_render_tier_b.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                                        C.c_void_p, C.c_void_p, C.POINTER(Stats)]
+        L.ro_render_tier_a_ex.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3, C.c_uint32,
+                                          C.c_uint32, C.c_uint32, C.c_uint32, U64x4, C.c_void_p, C.c_void_p,
+                                          C.POINTER(Stats), C.c_uint32, C.c_uint32]
         L.ro_quantize.restype = C.c_uint8
         L.ro_quantize.argtypes = [C.c_double, C.c_double]
         _lib = L
@@ -216,6 +220,86 @@ def render_tier_a(scene: Scene, cam: Camera, rng: ZigRandom, width: int, height:
                            depth, rng.s, out.ctypes.data, sums.ctypes.data if want_sum else None,
                            C.byref(st))
     return out, sums, st.as_dict()
+
+
+# ----------------------------------------------- README image (pin) ----
+# The reference's committed README image (RayTracingInOneWeekend.png, 600x400)
+# is a render of an EARLIER revision of generateRandomScene: the scene of the
+# book's first volume.  These restate that revision with the same Zig RNG
+# restatement, so the image pins the restated DefaultPrng stream (Xoshiro256++
+# seeded by SplitMix64, Random.float(f64)), the scene builder's draw order and
+# Tier A's camera / sphere / material arithmetic (tests/test_readme_image.py).
+BOOK1_SKY, BOOK1_NO_TIME = 1, 2  # rtw_oracle.h RO_BOOK1_*
+
+
+def readme_scene(seed: int = 42, f64=None):
+    """generateRandomScene (main.zig:157-221) as the README image has it: the
+    draw order of main.zig:177-218 (choose_mat, center.x, center.z, then
+    random01 * random01 albedo / metal albedo + fuzz) on a 22x22 grid
+    (a, b in [-11, 11)), static spheres (no center1 draw), a grey Lambertian
+    ground (0.5) and the three big spheres after the grid.  Returns the scene
+    and the DefaultPrng stream positioned after the build (main.zig:300-301:
+    the render continues the same stream)."""
+    rng = ZigRandom(seed)
+    draw = (lambda: f64(rng)) if f64 else rng.f64  # f64: an alternative float conversion (tests' control)
+    sph, mats = [], []
+
+    def add(c, r, kind, albedo=(0.0, 0.0, 0.0), fuzz=0.0, ir=0.0):
+        mats.append((kind, albedo, fuzz, ir))
+        sph.append((c, r, len(mats) - 1))
+
+    add((0.0, -1000.0, 0.0), 1000.0, LAMBERT_SOLID, (0.5, 0.5, 0.5))
+    for a in range(-11, 11):
+        for b in range(-11, 11):
+            choose = draw()
+            c = (a + 0.9 * draw(), 0.2, b + 0.9 * draw())
+            dx, dy, dz = c[0] - 4.0, c[1] - 0.2, c[2] - 0.0  # center.sub(4, 0.2, 0).norm() (vec.zig:12-18)
+            if math.sqrt(dx * dx + dy * dy + dz * dz) <= 0.9:
+                continue
+            if choose < 0.8:
+                a1 = [draw() for _ in range(3)]
+                a2 = [draw() for _ in range(3)]
+                add(c, 0.2, LAMBERT_SOLID, tuple(x * y for x, y in zip(a1, a2)))
+            elif choose < 0.95:
+                albedo = tuple(0.5 + draw() * 0.5 for _ in range(3))
+                add(c, 0.2, METAL, albedo, 0.0 + draw() * 0.5)
+            else:
+                add(c, 0.2, DIELECTRIC, ir=1.5)
+    add((0.0, 1.0, 0.0), 1.0, DIELECTRIC, ir=1.5)
+    add((-4.0, 1.0, 0.0), 1.0, LAMBERT_SOLID, (0.4, 0.2, 0.1))
+    add((4.0, 1.0, 0.0), 1.0, METAL, (0.7, 0.6, 0.5), 0.0)
+    sc = Scene()
+    sc.n_spheres, sc.n_mats = len(sph), len(mats)
+    for i, (c, r, m) in enumerate(sph):
+        q = sc.spheres[i]
+        q.c0[:], q.c1[:], q.radius, q.t0, q.t1, q.moving, q.mat = c, c, r, 0.0, 1.0, 0, m
+    for i, (k, albedo, fuzz, ir) in enumerate(mats):
+        q = sc.mats[i]
+        q.kind, q.fuzz, q.ir = k, fuzz, ir
+        q.albedo[:], q.albedo_odd[:] = albedo, albedo
+    return sc, rng
+
+
+def readme_camera() -> Camera:
+    """Camera.init (main.zig:52-89) of the README image: 3:2, vfov 20,
+    aperture 0.1, focus 10, looking at the origin from (12, 2, 3) — fitted
+    to the image (the current scene 1 looks from (13, 2, 3))."""
+    cam = Camera()
+    arr = C.c_double * 3
+    lib().ro_camera_init(C.byref(cam), arr(12, 2, 3), arr(0, 0, 0), arr(0, 1, 0), 20.0, 1.5, 0.1, 10.0, 0.0, 1.0)
+    return cam
+
+
+def render_tier_a_ex(scene: Scene, cam: Camera, rng: ZigRandom, width: int, height: int, spp: int,
+                     depth: int = 50, flags: int = BOOK1_SKY | BOOK1_NO_TIME, rows: int | None = None, bg=COVER_BG):
+    """Tier A with the README revision's differences (flags: gradient sky of the
+    book's first volume, no shutter-time draw); `rows` renders only the first
+    rows of the loop (j = 0.. : the bottom image rows)."""
+    out = np.zeros((height, width, 3), np.uint8)
+    st = Stats()
+    lib().ro_render_tier_a_ex(C.byref(scene), C.byref(cam), (C.c_double * 3)(*bg), width, height, spp, depth,
+                              rng.s, out.ctypes.data, None, C.byref(st), flags, height if rows is None else rows)
+    return out, st.as_dict()
 
 
 def render_tier_b(scene: Scene, cam: Camera, width: int, height: int, spp: int, depth: int = 50,
