@@ -67,7 +67,7 @@ def parse_args(argv=None):
     ap.add_argument("--width", type=int, default=W_IMG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32-variant", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=16, help="spp of the bounded CPU sample")
+    ap.add_argument("--cpu-spp", type=int, default=64, help="spp of the bounded CPU sample (~15-25 s on one core)")
     return ap.parse_args(argv)
 
 
@@ -75,10 +75,20 @@ def parse():
     return parse_args()
 
 
+def evidence(name):
+    """Path of a committed PMC evidence file: this round's (profiles/r02)
+    when present, else round 1's."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(REPO, "profiles", rnd, name)
+        if os.path.exists(path):
+            return path
+    return os.path.join(REPO, "profiles", "r01", name)
+
+
 def traffic_per_launch(args, W, H, spp):
     """HBM bytes per trace launch from the committed PMC passes of the same
-    config (profiles/r01/traffic.json, tools/gpu_bench_profile.sh), else None."""
-    path = os.path.join(REPO, "profiles", "r01", "traffic.json")
+    config (evidence("traffic.json"), tools/gpu_bench_profile.sh), else None."""
+    path = evidence("traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
@@ -91,10 +101,10 @@ def traffic_per_launch(args, W, H, spp):
 
 def valu_issue(args, W, H, spp):
     """VALU-issue evidence of the same config from the committed PMC passes
-    (profiles/r01/valu_issue.json, tools/gpu_pmc_valu.sh + tools/valu_json.py),
+    (evidence("valu_issue.json"), tools/gpu_pmc_valu.sh + tools/valu_json.py),
     else None: the share of SIMD cycles the VALU issues and the VALU
     instructions per wave-iteration (one bounce segment per lane)."""
-    path = os.path.join(REPO, "profiles", "r01", "valu_issue.json")
+    path = evidence("valu_issue.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
@@ -103,15 +113,15 @@ def valu_issue(args, W, H, spp):
     if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision):
         return None
     return {"busy_frac": t["valu_busy_frac"], "valu_per_wave_iteration": t["valu_per_wave_iteration"],
-            "variant": t.get("variant"), "source": "profiles/r01/valu_issue.json (PMC SQ_ACTIVE_INST_VALU, "
+            "variant": t.get("variant"), "source": os.path.relpath(path, REPO) + " (PMC SQ_ACTIVE_INST_VALU, "
             "SQ_INSTS_VALU of one launch)"}
 
 
 def wf_traffic(args, W, H, rc, spp):
     """HBM bytes of one wavefront frame (every wf_extend + wf_shade launch) from
-    the committed PMC passes of the same config (profiles/r01/wf_traffic.json,
+    the committed PMC passes of the same config (evidence("wf_traffic.json"),
     tools/gpu_pmc_wf.sh), else None."""
-    path = os.path.join(REPO, "profiles", "r01", "wf_traffic.json")
+    path = evidence("wf_traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
@@ -156,6 +166,34 @@ def cpu_baseline(width, height, spp_sample):
     return res
 
 
+def world_roofline(scene, s, kernel_ms, info):
+    """Roofline of the world kernel: VALU issue.  Its records are wave-uniform
+    scalar loads (no per-lane byte stream to price against HBM), so the roof
+    is the SIMDs' instruction issue: 1024 SIMDs x clock / 4 cycles per wave64
+    VALU instruction.  achieved = the VALU instructions of one launch (PMC
+    SQ_INSTS_VALU of the same config, profiles/r02/world_pmc_<scene>.json,
+    tools/gpu_world_pmc.sh + tools/world_pmc_json.py) / the launch time
+    measured here; traffic = its PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE."""
+    path = os.path.join(REPO, "profiles", "r02", f"world_pmc_{scene}.json")
+    bound = ("valu-issue (wave-uniform scalar-loaded records" +
+             ("; wave-cooperative BVH traversal)" if info["nodes"] else "; linear list, no BVH)"))
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return {"bound": bound, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    if f"{s.width}x{s.height}x{s.spp}" not in t["what"]:
+        return {"bound": bound, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    insts = t["counters"]["SQ_INSTS_VALU"]
+    achieved = insts / (kernel_ms * 1e-3) / 1e9
+    peak = 1024 * t["clock_ghz"] / 4
+    return {"bound": bound, "achieved": round(achieved, 1), "peak": round(peak, 1),
+            "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4),
+            "traffic": round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"]),
+            "valu_busy_frac_pmc": t["valu_busy_frac"], "wait_frac_of_wave_cycles": t["wait_frac_of_wave_cycles"],
+            "valu_per_wave_iteration": t["valu_per_wave_iteration"], "kernel": "world_kernel",
+            "source": f"profiles/r02/world_pmc_{scene}.json"}
+
+
 def world_variant(R, torch, scene, steps, warmup):
     """A general-world scene on the world kernel (csrc/rtw_world.hip) at the
     scene's own main.zig settings: scene 6 (Cornell box, the reference's
@@ -192,19 +230,7 @@ def world_variant(R, torch, scene, steps, warmup):
     info = dw.bvh_info()
     dw.close()
     samples = s.width * s.height * s.spp
-    if info["nodes"] == 0:  # linear world: wave-uniform scalar record loads, no per-lane data movement
-        roof = {"bound": "issue/latency (wave-uniform scalar-loaded records; no BVH)", "achieved": None,
-                "unit": None, "peak": None, "frac": None}
-    else:
-        # Wave-cooperative traversal: node (64 B) and primitive (128 B) records
-        # are wave-uniform scalar loads, so no per-lane byte stream exists to
-        # price against HBM; report the lane-level box-pair and primitive
-        # tests per second (the counters are per active lane).
-        tests = c["node_visits"] + c["prim_tests"]
-        roof = {"bound": "issue (wave-cooperative BVH traversal; wave-uniform scalar-loaded records, "
-                         "L2/MALL-resident; no HBM stream)",
-                "achieved": round(tests / (ms * 1e-3) / 1e9, 1), "unit": "G lane-tests/s (node pair + primitive)",
-                "peak": None, "frac": None}
+    roof = world_roofline(scene, s, ms, info)
     return {"value": round(samples * steps / e / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(e / steps * 1e3, 3),
             "kernel_ms": round(ms, 3), "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
                                                   "height": s.height, "spp": s.spp, "max_depth": DEPTH},

@@ -103,11 +103,6 @@ __device__ __forceinline__ R sqrt_k(R x) {
 constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
 constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
 __device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
-#ifdef RTW_RNG_FAST  // experiment: 32-bit folds (one VALU op each on 32-bit lanes)
-  z = (z ^ (z >> 32)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 32)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 32);
-#endif
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
