@@ -296,6 +296,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
+                         "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
                          "kernel": "wf_extend + wf_shade (all bounce launches of one frame) + wf_finish",
                          "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts,
                          "drain_segment_frac": round(drain, 4)},
@@ -486,6 +487,7 @@ def main():
             "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved_tf / peak, 4),
             "traffic": traffic_per_launch(args, W, H, spp),
+            "traffic_source": os.path.relpath(evidence("traffic.json"), REPO),
             "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
             "flop_per_launch": flops, "segments_per_launch": counts["segments"],
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",

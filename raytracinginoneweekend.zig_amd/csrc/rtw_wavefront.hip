@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
 // fast f64 sqrt (kVarFastSqrt), and a waves-per-SIMD target for the register
 // allocator (kWfExtendOcc, chosen by A/B on MI355X).
 #ifndef RTW_WF_EXT_OCC
-#define RTW_WF_EXT_OCC 6
+#define RTW_WF_EXT_OCC 5  // 6 measured 4 % faster per launch but spills 44 B/lane (wf_extend PMC traffic 104 vs 60 GB/frame)
 #endif
 constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
 template <typename R>

@@ -1,20 +1,33 @@
-"""The committed bench line (profiles/r01/bench.json, written by bench.py on an
+"""The committed bench line (profiles/r02/bench.json, written by bench.py on an
 MI355X) keeps the driver's contract: the BASELINE metric and unit, whole-job
 throughput consistent with ms_per_step, the roofline object (bound, achieved,
 peak, unit, frac = achieved / peak, traffic from the PMC passes) with the
-VALU-issue evidence of profiles/r01/valu_issue.json, and a bounded
+VALU-issue evidence of profiles/r02/valu_issue.json, the world kernels'
+VALU-issue rooflines (profiles/r02/world_pmc_*.json), and a bounded
 cpu_baseline.  CPU-only: it reads files, it runs nothing."""
 import json
 import os
 
 from conftest import REPO
 
-BENCH = os.path.join(REPO, "profiles", "r01", "bench.json")
+ROUND = "r02"
+BENCH = os.path.join(REPO, "profiles", ROUND, "bench.json")
 
 
-def load(name):
-    with open(os.path.join(REPO, "profiles", "r01", name)) as f:
+def load(name, rnd=ROUND):
+    with open(os.path.join(REPO, "profiles", rnd, name)) as f:
         return json.load(f)
+
+
+def source_round(roof, name, key):
+    """The round directory whose evidence file the bench line read (lines
+    without a traffic_source field: the round whose file holds the value)."""
+    if "traffic_source" in roof:
+        return roof["traffic_source"].split("/")[1]
+    for rnd in (ROUND, "r01"):
+        if os.path.exists(os.path.join(REPO, "profiles", rnd, name)) and round(load(name, rnd)[key]) == roof["traffic"]:
+            return rnd
+    return ROUND
 
 
 def test_bench_line_contract():
@@ -39,7 +52,7 @@ def test_roofline_fields_are_consistent():
     assert r["unit"] == "TFLOP/s" and r["peak"] == 78.6
     # achieved = algorithmic flops per launch / the launch's average duration
     assert abs(r["achieved"] - r["flop_per_launch"] / (r["trace_ms_per_launch"] * 1e-3) / 1e12) < 0.01 * r["achieved"]
-    t = load("traffic.json")
+    t = load("traffic.json", source_round(r, "traffic.json", "traffic_bytes_per_launch"))
     assert r["traffic"] == round(t["traffic_bytes_per_launch"])
     v = load("valu_issue.json")
     assert r["valu_issue"]["busy_frac"] == v["valu_busy_frac"]
@@ -52,7 +65,7 @@ def test_roofline_fields_are_consistent():
 def test_rocprof_summary_agrees_with_the_event_timing():
     import csv
     r = load("bench.json")["roofline"]
-    rows = list(csv.DictReader(open(os.path.join(REPO, "profiles", "r01", "bench_kernel_stats.csv"))))
+    rows = list(csv.DictReader(open(os.path.join(REPO, "profiles", ROUND, "bench_kernel_stats.csv"))))
     trace = [x for x in rows if x["Name"].startswith("void rtwk::trace_kernel<double, false, 0,")]
     assert trace, "no f64 trace_kernel row in the rocprofv3 summary"
     avg_ms = float(trace[0]["AverageNs"]) / 1e6
@@ -67,8 +80,24 @@ def test_cpu_baseline_is_bounded_and_stated():
 
 def test_wavefront_traffic_is_the_pmc_measurement():
     wf = load("bench.json")["wavefront_variant"]["roofline"]
-    t = load("wf_traffic.json")
+    t = load("wf_traffic.json", source_round(wf, "wf_traffic.json", "traffic_bytes_per_frame"))
     assert wf["traffic"] == round(t["traffic_bytes_per_frame"])
     # the queues move close to their algorithmic bytes (no wasted re-reads)
     assert 0.8 < wf["traffic"] / wf["algorithmic_bytes_per_frame"] < 1.5
     assert abs(wf["frac"] - wf["achieved"] / wf["peak"]) < 1e-3
+
+
+def test_world_rooflines_are_the_pmc_evidence():
+    b = load("bench.json")
+    for key, scene in (("globe_10k_variant", 7), ("cornell_variant", 6)):
+        r = b[key]["roofline"]
+        t = load(f"world_pmc_{scene}.json")
+        assert r["unit"] == "G wave64 VALU instructions/s" and r["kernel"] == "world_kernel"
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and 0.3 < r["frac"] <= 1.0
+        # achieved = the launch's PMC VALU instructions / the launch time measured by the bench
+        kms = b[key]["kernel_ms"]
+        assert abs(r["achieved"] - t["counters"]["SQ_INSTS_VALU"] / (kms * 1e-3) / 1e9) < 0.01 * r["achieved"]
+        assert abs(r["peak"] - 1024 * t["clock_ghz"] / 4) < 0.1
+        assert r["traffic"] == round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"])
+        # the PMC dispatch and the bench's launch time agree
+        assert abs(t["dispatch_ms"] - kms) / kms < 0.1
