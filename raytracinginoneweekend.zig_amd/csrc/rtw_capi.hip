@@ -94,6 +94,8 @@ struct rtw_scene_s {
   uint32_t n = 0, nm = 0, ng = 0;
   uint32_t n_static = 0, n_moving = 0, n_wide = 0;
   void* buf = nullptr;  // one allocation holding every table
+  std::vector<std::pair<double, double>> groups;  // moving-sphere time groups (t0, t1)
+  float cull_cmax_cl = 0.0f;                       // Cmax over members and cluster centres
   rtwk::SceneView<double> v64{};
   rtwk::SceneView<float> v32{};
 };
@@ -263,6 +265,104 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   const float cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
   const float rho = std::nextafter((float)rho_max, INFINITY);
   const uint32_t cull_on = (nn > 0 && cmax <= rtwc::kCmaxLimit) ? 1u : 0u;
+  // Clustered pretest tables (SceneView ccull..., trace VAR kVarCluster).
+  // kd-split of the narrow spheres (by the centre of their swept box over
+  // the shutter) into clusters of <= 8; members static first, so pairs are
+  // static-static where possible.  Bounding sphere of cluster c: centre
+  // C = f32(centre of the members' swept box), radius R = max over members
+  // of max(|c0 - C|, |c1 - C|) + |r|, widened by 1e-4 (1 + R): a line whose
+  // f64 discriminant for (C, R) is negative passes every member at a distance
+  // above its radius + 1e-4, far beyond the f64 rounding of the member's own
+  // exact test, which therefore rejects it.  Valid for
+  // sphere times within each time group's [t0, t1] (checked per render).
+  std::vector<uint32_t> cl_items;  // j (narrow index) per slot, ~0u = dummy
+  std::vector<float> cclus;
+  double cmax_cl = 0.0, rho_cl = 1.0;
+  {
+    auto cen_of = [&](uint32_t j, int k) {
+      const uint32_t pos = j < n_sn ? g_end[0] + j : g_end[2] + (j - n_sn);
+      const double* r = &sph64[8 * pos];
+      return r[k] + 0.5 * r[3 + k];
+    };
+    std::vector<std::vector<uint32_t>> groups;
+    std::vector<uint32_t> all(nn);
+    for (uint32_t j = 0; j < nn; ++j) all[j] = j;
+    if (nn) groups.push_back(all);
+    for (bool again = true; again;) {
+      again = false;
+      for (size_t gi = 0; gi < groups.size(); ++gi) {
+        if (groups[gi].size() <= rtwk::kClusterSlots) continue;
+        std::vector<uint32_t> g = groups[gi];
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t j : g)
+          for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], cen_of(j, k)), hi[k] = std::max(hi[k], cen_of(j, k));
+        int ax = 0;
+        for (int k = 1; k < 3; ++k)
+          if (hi[k] - lo[k] > hi[ax] - lo[ax]) ax = k;
+        std::stable_sort(g.begin(), g.end(), [&](uint32_t a, uint32_t b) { return cen_of(a, ax) < cen_of(b, ax); });
+        // Split sizes: whole clusters of 8 on the left, ceil(n/8) clusters in
+        // all (profiles/r02/cluster_ab.txt: fewer, fuller clusters beat
+        // smaller ones whose bounds are tighter: each cluster costs a ballot
+        // and a branch per wave-iteration).
+        constexpr size_t CS = rtwk::kClusterSlots;
+        const size_t h = CS * (((g.size() + CS - 1) / CS) / 2);
+        groups[gi].assign(g.begin(), g.begin() + h);
+        groups.emplace_back(g.begin() + h, g.end());
+        again = true;
+      }
+    }
+    for (auto& g : groups) {
+      std::stable_sort(g.begin(), g.end(), [&](uint32_t a, uint32_t b) { return (a >= n_sn) < (b >= n_sn); });
+      double mc0[rtwk::kClusterSlots][3], mdc[rtwk::kClusterSlots][3], mr[rtwk::kClusterSlots];
+      for (size_t i = 0; i < g.size(); ++i) {
+        const uint32_t pos = g[i] < n_sn ? g_end[0] + g[i] : g_end[2] + (g[i] - n_sn);
+        for (int k = 0; k < 3; ++k) mc0[i][k] = sph64[8 * pos + k], mdc[i][k] = sph64[8 * pos + 3 + k];
+        mr[i] = rad64[pos];
+      }
+      float cf[3], rf;
+      rtwc::cluster_sphere(mc0, mdc, mr, (int)g.size(), cf, rf);
+      const size_t c = cl_items.size() / rtwk::kClusterSlots;
+      if (cclus.size() < 16 * (c / 2 + 1)) cclus.resize(16 * (c / 2 + 1), 0.0f);
+      float* q = &cclus[16 * (c / 2) + (c & 1)];
+      for (int k = 0; k < 3; ++k) q[2 * k] = cf[k], cmax_cl = std::max(cmax_cl, (double)std::fabs(cf[k]));
+      q[12] = -(rf * rf);
+      rho_cl = std::max(rho_cl, 2.0 * (double)rf * (double)rf + 1.0);
+      for (uint32_t i = 0; i < rtwk::kClusterSlots; ++i) cl_items.push_back(i < g.size() ? g[i] : ~0u);
+    }
+  }
+  const uint32_t n_clusters = (uint32_t)(cl_items.size() / rtwk::kClusterSlots);
+  const uint32_t n_cslots = rtwk::kClusterSlots * n_clusters;
+  // slot tables; a dummy slot's record (c = 0, nr2 = +3e38) is a proven miss for every lane
+  std::vector<float> ccull((size_t)8 * n_cslots + 16, 0.0f);
+  std::vector<uint32_t> ccull_tg(n_cslots / 2 + 1, 0u), cpos(std::max(n_cslots, 1u), 0u);
+  std::vector<uint32_t> cvalid(2 * ((n_cslots + 63) / 64) + 2, 0u);
+  for (uint32_t sl = 0; sl < n_cslots; ++sl) {
+    float* q = &ccull[(size_t)16 * (sl / 2) + (sl & 1)];
+    const uint32_t j = cl_items[sl];
+    if (j == ~0u) {
+      q[12] = 3e38f;
+      continue;
+    }
+    const uint32_t pos = j < n_sn ? g_end[0] + j : g_end[2] + (j - n_sn);
+    const float* src = &cull[(size_t)16 * (j / 2) + (j & 1)];  // the member's own pretest record
+    for (int k = 0; k < 7; ++k) q[2 * k] = src[2 * k];
+    cpos[sl] = pos;
+    cvalid[2 * (sl / 64) + ((sl % 64) >> 5)] |= 0x80000000u >> (sl & 31u);
+    const uint32_t g = (meta[pos] & rtwk::kMoving) ? (meta[pos] >> 2) & 63u : 0u;
+    ccull_tg[sl / 2] |= g << (8 * (sl & 1));
+  }
+  for (uint32_t p = 0; p < n_cslots / 2; ++p) {
+    const uint32_t j0 = cl_items[2 * p], j1 = cl_items[2 * p + 1];
+    const bool m0 = j0 != ~0u && j0 >= n_sn, m1 = j1 != ~0u && j1 >= n_sn;
+    if (!m0 && !m1) ccull_tg[p] |= 1u << 17;  // static pair (dummies count as static)
+    if (!m0 && m1) ccull_tg[p] = (ccull_tg[p] & 0xFF00u) | ((ccull_tg[p] >> 8) & 0xFFu) | (ccull_tg[p] & ~0xFFFFu);
+    if (m0 && !m1) ccull_tg[p] = (ccull_tg[p] & 0xFFu) | ((ccull_tg[p] & 0xFFu) << 8) | (ccull_tg[p] & ~0xFFFFu);
+    const float* q = &ccull[(size_t)16 * p];
+    if (q[6] == 0.0f && q[7] == 0.0f && q[10] == 0.0f && q[11] == 0.0f) ccull_tg[p] |= 1u << 16;
+  }
+  if (cclus.empty()) cclus.assign(16, 0.0f);
+  const float cmax_all = std::max(cmax, std::nextafter((float)cmax_cl, INFINITY));
+  const float rho_c = std::nextafter((float)rho_cl, INFINITY);
   // One device allocation, 256-B aligned sub-buffers.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   size_t off = 0;
@@ -277,6 +377,8 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   const size_t o_mat32 = place(mat32.size() * 4), o_tg32 = place(tg32.size() * 4);
   const size_t o_meta = place(meta.size() * 4), o_kind = place(kind.size() * 4), o_perm = place(perm.size() * 4);
   const size_t o_cull = place(cull.size() * 4), o_cull_tg = place(cull_tg.size() * 4);
+  const size_t o_ccull = place(ccull.size() * 4), o_ccull_tg = place(ccull_tg.size() * 4);
+  const size_t o_cclus = place(cclus.size() * 4), o_cpos = place(cpos.size() * 4), o_cvalid = place(cvalid.size() * 4);
   const size_t total = off;
   std::vector<unsigned char> host(total, 0);
   auto cp = [&](size_t o, const void* p, size_t bytes) {
@@ -295,6 +397,11 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   cp(o_perm, perm.data(), perm.size() * 4);
   cp(o_cull, cull.data(), cull.size() * 4);
   cp(o_cull_tg, cull_tg.data(), cull_tg.size() * 4);
+  cp(o_ccull, ccull.data(), ccull.size() * 4);
+  cp(o_ccull_tg, ccull_tg.data(), ccull_tg.size() * 4);
+  cp(o_cclus, cclus.data(), cclus.size() * 4);
+  cp(o_cpos, cpos.data(), cpos.size() * 4);
+  cp(o_cvalid, cvalid.data(), cvalid.size() * 4);
 
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -317,12 +424,17 @@ int rtw_scene_create(const rtw_sphere* spheres, uint32_t n, const rtw_material* 
   auto D = [&](size_t o) { return reinterpret_cast<const double*>(b + o); };
   auto F = [&](size_t o) { return reinterpret_cast<const float*>(b + o); };
   auto U = [&](size_t o) { return reinterpret_cast<const uint32_t*>(b + o); };
+  // cluster_on (per render, fill_args): usable when the scene's bound allows (cmax_all within the limit)
+  const uint32_t cl_ok = (n_clusters > 0 && cull_on && cmax_all <= rtwc::kCmaxLimit) ? 1u : 0u;
   sc->v64 = {D(o_sph64), D(o_rad64), U(o_meta), D(o_mat64), U(o_kind), D(o_tg64), D(o_sph64), D(o_tg64), U(o_perm),
              F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
-             cmax, rho};
+             cl_ok ? cmax_all : cmax, rho, F(o_ccull), U(o_ccull_tg), F(o_cclus), U(o_cpos), U(o_cvalid), n_clusters,
+             cl_ok, rho_c};
   sc->v32 = {F(o_sph32), F(o_rad32), U(o_meta), F(o_mat32), U(o_kind), F(o_tg32), D(o_sph64), D(o_tg64), U(o_perm),
              F(o_cull), U(o_cull_tg), F(o_tg32), n, nm, ng, g_end[0], g_end[1], g_end[2], nn, nn_pad, n_sn, cull_on,
-             cmax, rho};
+             cmax, rho, F(o_ccull), U(o_ccull_tg), F(o_cclus), U(o_cpos), U(o_cvalid), n_clusters, 0u, rho_c};
+  sc->cull_cmax_cl = cmax_all;
+  sc->groups = groups;
   *out = sc;
   return RTW_OK;
 }
@@ -456,7 +568,17 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
 size_t lds_bytes(const rtw_scene_s* sc, int prec) {
   const size_t r = prec == 1 ? 4 : 8;
   return rtwk::kCoopLdsBytes + r * (8 * ((size_t)sc->n + 1) + (size_t)sc->n + 8 * (size_t)sc->nm + 4 * (size_t)sc->ng) +
-         4 * ((size_t)sc->n + 1 + sc->nm + sc->n) + 16;
+         4 * ((size_t)sc->n + 1 + sc->nm + sc->n + rtwk::kClusterSlots * (size_t)sc->v64.n_clusters) + 16;
+}
+
+// The clustered pretest's bounding spheres hold each moving member over its
+// time group's [t0, t1]: usable only when the camera's shutter lies inside
+// every group's range (else the members' centres leave the bounds).
+uint32_t clusters_usable(const rtw_scene_s* sc, const rtw_camera* cam) {
+  if (!sc->v64.cluster_on) return 0u;
+  for (const auto& g : sc->groups)
+    if (!(cam->time0 >= g.first && cam->time1 <= g.second)) return 0u;
+  return 1u;
 }
 
 // ---------------------------------------------------------- wavefront ----
@@ -689,6 +811,7 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   } else {
     rtwk::TraceArgs<double> a;
     fill_args(a, sc->v64, cam, p, ws, L);
+    a.sc.cluster_on = clusters_usable(sc, cam);
     total_units = a.total_units;
     const uint32_t want = (total_units + 255) / 256;
     const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
@@ -775,7 +898,9 @@ int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* 
   HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
   if (mode == 1 && getenv("RTW_COUNTS_VERBOSE")) {
     fprintf(stderr, "[rtw counts] samples %llu segments %llu skipped %llu cand_wave_iters %llu cand_lanes %llu "
-            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
+            "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu "
+            "cluster_wave_tests %llu cluster_wave_skips %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8],
+            st[11], st[12]);
   }
   if (mode == 2) {
     const char* names[10] = {"refill",  "start_sample", "wide+pretest", "hit+kind",    "tail",

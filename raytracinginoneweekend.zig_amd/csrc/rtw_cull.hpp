@@ -74,4 +74,38 @@ RTWC_HD float cull_x(float ox, float oy, float oz, float dx, float dy, float dz,
   return std::fma(lk.na, cc, std::fma(hb, hb, lk.k));
 }
 
+// Bounding sphere of a cluster of n (possibly moving) narrow spheres for the
+// clustered pretest (trace VAR kVarCluster; host only).  Member i: centre
+// c0_i + f * dc_i for f in [0, 1] (the shutter inside its time group),
+// radius |r_i|.  Centre cf = f32 of the centre of the members' swept box;
+// radius R = max_i max(|c0_i - cf|, |c0_i + dc_i - cf|) + |r_i|, widened by
+// 1e-4 (1 + R) and rounded up to f32.  A line whose f64 discriminant against
+// (cf, rf) is negative passes each member's centre farther than |r_i| +
+// ~1e-4 (1 + R): the member's own f64 discriminant (rounding ~1e-15 relative)
+// is then negative too, so the cull_x proof for (cf, rf) proves every member
+// missed.  tests/test_cull_host.py checks it on adversarial clusters.
+inline void cluster_sphere(const double (*c0)[3], const double (*dc)[3], const double* r, int n, float cf[3],
+                           float& rf) {
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k)
+      for (int e = 0; e < 2; ++e) {
+        const double c = c0[i][k] + (e ? dc[i][k] : 0.0);
+        lo[k] = std::fmin(lo[k], c - std::fabs(r[i]));
+        hi[k] = std::fmax(hi[k], c + std::fabs(r[i]));
+      }
+  for (int k = 0; k < 3; ++k) cf[k] = (float)(0.5 * (lo[k] + hi[k]));
+  double R = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double d0 = 0.0, d1 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      d0 += (c0[i][k] - cf[k]) * (c0[i][k] - cf[k]);
+      d1 += (c0[i][k] + dc[i][k] - cf[k]) * (c0[i][k] + dc[i][k] - cf[k]);
+    }
+    R = std::fmax(R, std::sqrt(std::fmax(d0, d1)) + std::fabs(r[i]));
+  }
+  R = R + 1e-4 * (1.0 + R);
+  rf = std::nextafter((float)R, INFINITY);
+}
+
 }  // namespace rtwc

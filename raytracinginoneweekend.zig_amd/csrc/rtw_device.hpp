@@ -83,6 +83,10 @@ constexpr int kVarMergedStart = 262144;
 constexpr int kVarPreDraw = 524288;
 // Unit refill: each 64-unit batch's (tile, chunk) decoded once per batch.
 constexpr int kVarBatchDecode = 1048576;
+// f64 pretest over spatial clusters of narrow spheres (SceneView ccull...):
+// a wave skips a cluster's member pretests when every lane's line provably
+// misses the cluster's bounding sphere.
+constexpr int kVarCluster = 2097152;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
@@ -556,6 +560,7 @@ struct LdsTables {
   uint32_t* meta;
   uint32_t* kind;
   uint32_t* perm;  // original list index -> table position
+  uint32_t* cpos;  // clustered pretest: slot -> table position
 };
 template <typename R>
 __device__ __forceinline__ LdsTables<R> stage_tables(const SceneView<R>& S, unsigned char* lds_raw) {
@@ -568,6 +573,7 @@ __device__ __forceinline__ LdsTables<R> stage_tables(const SceneView<R>& S, unsi
   T.meta = reinterpret_cast<uint32_t*>(T.tg + 4 * S.ng);
   T.kind = T.meta + S.n + 1;
   T.perm = T.kind + S.nm;
+  T.cpos = T.perm + S.n;
   for (uint32_t i = threadIdx.x; i < 8 * (S.n + 1); i += blockDim.x) T.sph[i] = S.sph[i];
   for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) T.rad[i] = S.rad[i];
   for (uint32_t i = threadIdx.x; i < 8 * S.nm; i += blockDim.x) T.mat[i] = S.mat[i];
@@ -575,6 +581,7 @@ __device__ __forceinline__ LdsTables<R> stage_tables(const SceneView<R>& S, unsi
   for (uint32_t i = threadIdx.x; i < S.n + 1; i += blockDim.x) T.meta[i] = S.meta[i];
   for (uint32_t i = threadIdx.x; i < S.nm; i += blockDim.x) T.kind[i] = S.kind[i];
   for (uint32_t i = threadIdx.x; i < S.n; i += blockDim.x) T.perm[i] = S.perm[i];
+  for (uint32_t i = threadIdx.x; i < kClusterSlots * S.n_clusters; i += blockDim.x) T.cpos[i] = S.cpos[i];
   __syncthreads();
   return T;
 }
@@ -586,6 +593,7 @@ struct KStats {
   unsigned long long samples = 0, segments = 0, skipped = 0;
   unsigned long long candwave = 0, candlane = 0, disc = 0, wave_iters = 0;
   unsigned long long cull_lanes = 0, cull_iters = 0;
+  unsigned long long cl_tests = 0, cl_skips = 0;  // clustered pretest: (wave, cluster) pairs, skipped ones
   uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_last = 0;
 };
@@ -793,6 +801,116 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
         sk[h] = cnt == 0u ? 0u : (cnt == 32u ? sk[h] : sk[h] << (32u - cnt));
       }
     };
+    // Per lane: the exact test on the survivors of a 64-slot block (bit 31-r
+    // of m0 / m1 = slot base+r / base+32+r); `clustered`: slots of the
+    // clustered tables (T.cpos), else the narrow order of the cull table.
+    auto run_survivors = [&](uint32_t m0, uint32_t m1, uint32_t base, bool clustered) {
+        while (m0 | m1) {  // per lane: the exact test on the survivors
+          if constexpr (STATS) {
+            if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.cull_iters++;
+          }
+          uint32_t r;
+          if (m0) {
+            r = __clz(m0);
+            m0 &= ~(0x80000000u >> r);
+          } else {
+            r = __clz(m1);
+            m1 &= ~(0x80000000u >> r);
+            r += 32u;
+          }
+          const uint32_t j = base + r;
+          const uint32_t k = clustered ? T.cpos[j] : (j < S.n_sn ? S.g_static_wide + j : S.g_moving_wide + (j - S.n_sn));
+          const R* sp = T.sph + 8 * k;
+          const uint32_t meta = T.meta[k];
+          R cx = sp[0], cy = sp[1], cz = sp[2];
+          if (meta & kMoving) {
+            const int g = (int)((meta >> 2) & 63u);
+            if (g != fr_g) {  // per lane: usually once per segment
+              fr_g = g;
+              fr_v = rtwm::div_rn(L.time - T.tg[4 * g], T.tg[4 * g + 1] - T.tg[4 * g], T.tg[4 * g + 2]);
+            }
+            cx = cx + sp[3] * fr_v;
+            cy = cy + sp[4] * fr_v;
+            cz = cz + sp[5] * fr_v;
+          }
+          test(k, meta, cx, cy, cz, sp[6]);
+        }
+    };
+    bool clustered_done = false;
+    if constexpr ((VAR & kVarCluster) != 0 && !F32) {
+      if (S.cluster_on) {  // kernel argument: wave-uniform
+        clustered_done = true;
+        const f2 kcl = bc(lc.alpha * S.cull_rho_cl);
+        const RTW_CONST f2* cct = reinterpret_cast<const RTW_CONST f2*>(cptr(S.ccull));
+        const RTW_CONST f2* ccl = reinterpret_cast<const RTW_CONST f2*>(cptr(S.cclus));
+        const RTW_CONST uint32_t* cctg = cptr(S.ccull_tg);
+        const RTW_CONST uint32_t* cval = cptr(S.cvalid);
+        constexpr uint32_t CS = kClusterSlots, CPB = 64u / kClusterSlots;  // slots per cluster, clusters per block
+        for (uint32_t cb = 0; cb < S.n_clusters; cb += CPB) {  // one 64-slot block
+          const uint32_t nb = min(CPB, S.n_clusters - cb);
+          // cluster pretest (bounding spheres as static pair records): bit c = proven miss
+          uint32_t cmiss = 0u;
+          for (uint32_t q = 0; 2u * q < nb; ++q) {
+            const f2 x = cull_pair<0>(ld_pair(ccl, (cb >> 1) + q), ox, oy, oz, dx, dy, dz, na, kcl, bc(0.0f));
+            cmiss |= ((__float_as_uint(x.x) >> 31) << (2u * q)) | ((__float_as_uint(x.y) >> 31) << (2u * q + 1u));
+          }
+          if (!lc.ok) cmiss = 0u;
+          uint64_t sk64 = 0u;  // slot bits, cluster cb first (MSB side after the final shift)
+          uint32_t tgp_cur = ~0u;
+          f2 fr2 = bc(0.0f);
+#pragma unroll 1
+          for (uint32_t c = 0; c < nb; ++c) {
+            constexpr uint32_t kAll = (1u << CS) - 1u;
+            uint32_t b8 = kAll;  // every slot proven missed
+            const bool need = __ballot(((cmiss >> c) & 1u) == 0u) != 0;  // some lane's line may meet the cluster
+            if constexpr (STATS) {
+              if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) {
+                st.cl_tests++;
+                st.cl_skips += need ? 0u : 1u;
+              }
+            }
+            if (need) {
+              b8 = 0u;
+              const uint32_t p0 = (cb + c) * (CS / 2u);
+#pragma unroll
+              for (uint32_t i = 0; i < CS / 2u; ++i) {
+                const uint32_t p = p0 + i;
+                const PairRec rec = ld_pair(cct, p);
+                const uint32_t tgp = cctg[p];
+                f2 x;
+                if (tgp & (1u << 17)) {
+                  x = cull_pair<0>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                } else {
+                  if ((tgp & 0xFFFFu) != tgp_cur) {  // wave-uniform
+                    tgp_cur = tgp & 0xFFFFu;
+                    const uint32_t g0 = tgp & 0xFFu, g1 = (tgp >> 8) & 0xFFu;
+                    fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
+                  }
+                  x = (tgp & (1u << 16)) ? cull_pair<2>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2)
+                                         : cull_pair<1>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                }
+                b8 = __builtin_amdgcn_alignbit(b8, __float_as_uint(x.x), 31);
+                b8 = __builtin_amdgcn_alignbit(b8, __float_as_uint(x.y), 31);
+              }
+              b8 = (b8 & kAll) | (((cmiss >> c) & 1u) ? kAll : 0u);
+            }
+            sk64 = (sk64 << CS) | b8;
+          }
+          sk64 <<= CS * (CPB - nb);
+          const uint32_t sk[2] = {(uint32_t)(sk64 >> 32), (uint32_t)sk64};
+          uint32_t m0 = cval[2u * (cb / CPB)], m1 = cval[2u * (cb / CPB) + 1u];
+          if (lc.ok) {
+            m0 &= ~sk[0];
+            m1 &= ~sk[1];
+          }
+          if constexpr (STATS) st.cull_lanes += __popc(m0) + __popc(m1);
+          RTW_STAMP(2)
+          run_survivors(m0, m1, cb * CS, true);
+          RTW_STAMP(6)
+        }
+      }
+    }
+    if (!clustered_done)
     for (uint32_t base = 0; base < S.nn; base += 64) {
       uint32_t sk[2];
       pretest_block(base, ox, oy, oz, dx, dy, dz, sk);
@@ -813,36 +931,7 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
       }
       if constexpr (STATS) st.cull_lanes += __popc(m0) + __popc(m1);
       RTW_STAMP(2)
-      while (m0 | m1) {  // per lane: the exact test on the survivors
-        if constexpr (STATS) {
-          if (lid == (uint32_t)__builtin_ctzll(__ballot(true))) st.cull_iters++;
-        }
-        uint32_t r;
-        if (m0) {
-          r = __clz(m0);
-          m0 &= ~(0x80000000u >> r);
-        } else {
-          r = __clz(m1);
-          m1 &= ~(0x80000000u >> r);
-          r += 32u;
-        }
-        const uint32_t j = base + r;
-        const uint32_t k = j < S.n_sn ? S.g_static_wide + j : S.g_moving_wide + (j - S.n_sn);
-        const R* sp = T.sph + 8 * k;
-        const uint32_t meta = T.meta[k];
-        R cx = sp[0], cy = sp[1], cz = sp[2];
-        if (meta & kMoving) {
-          const int g = (int)((meta >> 2) & 63u);
-          if (g != fr_g) {  // per lane: usually once per segment
-            fr_g = g;
-            fr_v = rtwm::div_rn(L.time - T.tg[4 * g], T.tg[4 * g + 1] - T.tg[4 * g], T.tg[4 * g + 2]);
-          }
-          cx = cx + sp[3] * fr_v;
-          cy = cy + sp[4] * fr_v;
-          cz = cz + sp[5] * fr_v;
-        }
-        test(k, meta, cx, cy, cz, sp[6]);
-      }
+      run_survivors(m0, m1, base, false);
       RTW_STAMP(6)
     }
   }

@@ -51,7 +51,25 @@ struct SceneView {
   uint32_t cull_on;           // pretest usable for this scene (rtw_cull.hpp limits)
   float cull_cmax;            // max |c0|_inf + |c1 - c0|_inf over narrow spheres (rounded up)
   float cull_rho;             // max 2 r^2 + 1 over narrow spheres (rounded up)
+  // Clustered pretest (trace VAR kVarCluster, f64): the narrow spheres in
+  // spatial clusters of <= 8 slots (cluster c = slots 8c..8c+7, padded with
+  // dummy slots); a bounding sphere per cluster, pretested first, lets a wave
+  // skip every member's pretest when no lane's ray line can meet it.
+  const float* ccull;         // pair records in slot order (PairRec, 16 f32 per slot pair); kClusterSlots per cluster
+  const uint32_t* ccull_tg;   // per slot pair: time groups (bits 0-15), y-only (16), static pair (17)
+  const float* cclus;         // cluster bounding spheres as static pair records (2 clusters per record)
+  const uint32_t* cpos;       // slot -> table position (dummy slots: 0)
+  const uint32_t* cvalid;     // per 64-slot block: 2 words, bit 31 - r of word h = slot 32h + r real
+  uint32_t n_clusters;        // clusters (blocks of 8 -> 64 slots)
+  uint32_t cluster_on;        // clusters usable (set per render: camera times within every time group)
+  float cull_rho_cl;          // max 2 R^2 + 1 over the cluster bounding spheres (rounded up)
 };
+
+#ifndef RTW_CLUSTER_SLOTS  // (A/B builds override it: 4 or 8)
+#define RTW_CLUSTER_SLOTS 8
+#endif
+constexpr uint32_t kClusterSlots = RTW_CLUSTER_SLOTS;  // slots per cluster (even, divides 64)
+static_assert(kClusterSlots % 2 == 0 && 64 % kClusterSlots == 0, "cluster slots");
 
 template <typename R>
 struct TraceArgs {
@@ -93,9 +111,13 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 // of rtw_device.hpp / rtw_trace.hip, chosen by the in-process A/B on MI355X,
 // profiles/r01/ab_defaults.txt): scalar sphere records + 512 (scene fields from
 // the kernel argument) + kVarR0Table + kVarMergedStart + kVarPreDraw; f64 also
-// 4 waves/SIMD (4) + kVarFastSqrt, f32 5 waves/SIMD (8).  Every other variant
+// 4 waves/SIMD (4) + kVarFastSqrt + kVarCluster (round 2, +5.4 %,
+// profiles/r02/cluster_ab.txt), f32 5 waves/SIMD (8).  Every other variant
 // exists only in the -DRTW_MEASURE build.
-constexpr int kDefaultVarF64 = 4 + 512 + 32768 + 131072 + 262144 + 524288;  // 950788
+#ifndef RTW_DEFAULT_VAR_F64  // (A/B builds override it)
+#define RTW_DEFAULT_VAR_F64 (4 + 512 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3048452 (+ kVarCluster)
+#endif
+constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
 constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
 bool trace_variant_built(int precision, int var);
 constexpr int kTraceBlock = 256;

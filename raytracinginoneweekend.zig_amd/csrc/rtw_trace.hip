@@ -333,6 +333,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     atomicAdd(A.stats + 6, st.wave_iters);
     atomicAdd(A.stats + 7, st.cull_lanes);
     atomicAdd(A.stats + 8, st.cull_iters);
+    atomicAdd(A.stats + 11, st.cl_tests);
+    atomicAdd(A.stats + 12, st.cl_skips);
   }
   if constexpr (MODE == 2) {
     RTW_STAMP(4)

@@ -49,3 +49,28 @@ def test_check_detects_a_too_small_margin(tmp_path):
     exe = _build(tmp_path, str(weak))
     rc, _, _, viol = _run(exe, 2_000_000, 1)
     assert viol > 0 and rc == 1
+
+
+CLSRC = os.path.join(REPO, "tests", "cluster_bound_check.cpp")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_cluster_pretest_never_skips_a_member_that_can_be_hit(tmp_path):
+    """Clustered pretest (trace VAR kVarCluster, rtw_cull.hpp cluster_sphere):
+    a cluster proven missed has every member's exact f64 discriminant negative
+    (at every shutter time); with the bound radius shrunk by 2 % the check
+    finds violations (it has teeth)."""
+    exe = str(tmp_path / "clchk")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-I", CSRC, CLSRC, "-o", exe], check=True)
+
+    def run(n, seed, shrink="0"):
+        p = subprocess.run([exe, str(n), str(seed), shrink], capture_output=True, text=True)
+        m = re.search(r"cases (\d+) skipped (\d+) violations (\d+)", p.stdout)
+        assert m, p.stdout + p.stderr
+        return p.returncode, int(m.group(1)), int(m.group(2)), int(m.group(3))
+    for seed in (1, 2):
+        rc, cases, skipped, viol = run(400_000, seed)
+        assert viol == 0 and rc == 0
+        assert skipped > cases // 10  # the cluster pretest does skip
+    rc, cases, skipped, viol = run(400_000, 3, "0.02")
+    assert viol > 0
