@@ -115,7 +115,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 // profiles/r02/cluster_ab.txt), f32 5 waves/SIMD (8).  Every other variant
 // exists only in the -DRTW_MEASURE build.
 #ifndef RTW_DEFAULT_VAR_F64  // (A/B builds override it)
-#define RTW_DEFAULT_VAR_F64 (4 + 512 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3048452 (+ kVarCluster)
+#define RTW_DEFAULT_VAR_F64 (4 + 512 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3047940 (+ kVarCluster)
 #endif
 constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
 constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024

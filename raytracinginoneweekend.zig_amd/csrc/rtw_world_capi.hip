@@ -301,6 +301,16 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
+    if (getenv("RTW_BVH_DEBUG")) {  // root's two children: leaf (prims) or node, and their boxes
+      for (int c = 0; c < 2; ++c) {
+        uint32_t ref;
+        std::memcpy(&ref, bvh.nodes.data() + 12 + c, 4);
+        const float* nd = bvh.nodes.data();
+        fprintf(stderr, "[rtw bvh] root child %d: %s %u, box x [%g, %g] y [%g, %g] z [%g, %g]\n", c,
+                (ref & rtwk::kLeafBit) ? "leaf of" : "node", (ref & rtwk::kLeafBit) ? (ref >> 23) & rtwk::kLeafCountMask : ref,
+                nd[0 + c], nd[6 + c], nd[2 + c], nd[8 + c], nd[4 + c], nd[10 + c]);
+      }
+    }
   } else {
     for (uint32_t i = 0; i < d->n_prims; ++i) bvh.order.push_back(i);
   }

@@ -306,3 +306,23 @@ def test_cornell_oracle_geometry(oracle):
     wz = -math.sin(t) * cx + math.cos(t) * cz + 295
     h = w.hit((wx, 500, wz), (0, -1, 0))
     assert h is not None and abs(h["p"][1] - 330) < 1e-9 and abs(h["normal"][1] - 1) < 1e-12
+
+
+def test_globe_bvh_isolates_the_ground_at_the_root():
+    """configs[4]: the binned SAH puts the r=1000 ground sphere (box 2000 wide)
+    in a leaf of its own at the root and the globe + 10k spheres in the other
+    child (box ~100 x 4 x 100): the oversized primitive is already hoisted out
+    of the traversal (one test per segment), the rest never descends under a
+    scene-sized box.  (The builder runs before the device is needed.)"""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from rtw_amd import world as W\n"
+            "b = W.BuiltScene(7, 42, image=W.earth_map())\n"
+            "try:\n    W.DeviceWorld(b.desc).close()\nexcept Exception:\n    pass\n") % os.path.join(REPO, "raytracinginoneweekend.zig_amd")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, RTW_BVH_DEBUG="1"))
+    lines = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh] root child")]
+    assert len(lines) == 2, p.stderr
+    assert "leaf of 1, box x [-1000, 1000] y [-2000, 0] z [-1000, 1000]" in lines[0]
+    assert "node" in lines[1] and "y [0, 4]" in lines[1]
