@@ -127,8 +127,9 @@ def wf_traffic(args, W, H, rc, spp):
     except (OSError, ValueError):
         return None
     c = t.get("config", {})
+    fused = os.environ.get("RTW_WF_FUSED", "1") != "0"
     if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision) \
-            or rc != H or args.wf_paths != 0:
+            or rc != H or args.wf_paths != 0 or c.get("fused", False) != fused:
         return None
     return round(t["traffic_bytes_per_frame"])
 
@@ -243,16 +244,21 @@ def world_variant(R, torch, scene, steps, warmup):
 
 def wavefront_bytes(counts, precision, units):
     """Algorithmic HBM bytes of one wavefront frame (rtw_wavefront.hip): per
-    bounce segment, extend reads o, d, time (+ the skip word in f32) and
-    writes (root, winner); shade reads the path + (root, winner) and writes
-    the path.  Per sample: the home slot's unit, sample index and f64x3 sum
+    bounce segment of the fused engine (default), wf_step reads the path +
+    its hit (root, winner) and writes the next path + its hit; of the split
+    engine (RTW_WF_FUSED=0), extend reads o, d, time (+ the skip word in f32)
+    and writes (root, winner), shade reads the path + (root, winner) and
+    writes the path.  Per sample: the home slot's unit, sample index and f64x3 sum
     (read + write).  Per unit: the f64x3 chunk sum.  `counts` is the
     wavefront engine's own counts pass: segments traced by the in-register
     drain (wf_finish, counts["drain_segments"]) move no queue bytes (its one
     load of each live path, <= 96 B x slots, is left out: < 0.1 %)."""
     r = 8 if precision == "f64" else 4
     path = 10 * r + 8 + 4 + 4
-    seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
+    if os.environ.get("RTW_WF_FUSED", "1") != "0":  # fused engine: path + hit read, path + hit written
+        seg = 2 * (path + r + 4)
+    else:  # extend reads o, d, time (+ skip), writes the hit; shade reads path + hit, writes the path
+        seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
     queued = counts["segments"] - counts.get("drain_segments", 0)
     return queued * seg + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
 
@@ -297,7 +303,8 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
-                         "kernel": "wf_extend + wf_shade (all bounce launches of one frame) + wf_finish",
+                         "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
+                                   + " (all bounce launches of one frame) + wf_finish",
                          "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts,
                          "drain_segment_frac": round(drain, 4)},
             "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
@@ -503,7 +510,8 @@ def main():
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
-                    "kernel": "wf_extend + wf_shade (all bounce launches of one frame) + wf_finish",
+                    "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
+                                   + " (all bounce launches of one frame) + wf_finish",
                     "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,
                     "valu": {"achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                              "frac": round(achieved_tf / peak, 4)}}

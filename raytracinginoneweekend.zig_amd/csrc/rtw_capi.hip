@@ -503,8 +503,8 @@ struct WsLayout {
   size_t wf_off, total;
 };
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
-// Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk).
-size_t wf_queue_bytes(size_t n, size_t r) { return 10 * al256(n * r) + al256(n * 8) + 2 * al256(n * 4); }
+// Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk, + the fused engine's hit root, winner).
+size_t wf_queue_bytes(size_t n, size_t r) { return 11 * al256(n * r) + al256(n * 8) + 3 * al256(n * 4); }
 WsLayout ws_layout(const rtw_params* p) {
   WsLayout w;
   w.partial_off = 0;
@@ -598,6 +598,12 @@ struct WfLaunch<double> {
   static hipError_t fin(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_finish_f64(a, g, l, s, stats);
   }
+  static hipError_t gen_hit(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_generate_hit_f64(a, g, l, s);
+  }
+  static hipError_t step(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_step_f64(a, g, l, s, stats);
+  }
 };
 template <>
 struct WfLaunch<float> {
@@ -612,6 +618,12 @@ struct WfLaunch<float> {
   }
   static hipError_t fin(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_finish_f32(a, g, l, s, stats);
+  }
+  static hipError_t gen_hit(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
+    return rtwk::launch_wf_generate_hit_f32(a, g, l, s);
+  }
+  static hipError_t step(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_step_f32(a, g, l, s, stats);
   }
 };
 
@@ -628,6 +640,10 @@ rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
   q.slot = reinterpret_cast<uint32_t*>(b);
   b += al256(n * 4);
   q.dsk = reinterpret_cast<uint32_t*>(b);
+  b += al256(n * 4);
+  q.ht = reinterpret_cast<R*>(b);
+  b += al256(n * sizeof(R));
+  q.hk = reinterpret_cast<int32_t*>(b);
   b += al256(n * 4);
   return q;
 }
@@ -687,11 +703,15 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     const uint32_t per_cu = (uint32_t)wf_bpc(dev, (int)(sizeof(R) == 4), kernel, lds);
     return std::max(1u, std::min((uint32_t)device_cus(dev) * per_cu * gmul, max_grid));
   };
-  const uint32_t grid = grid_of(2), grid_ext = grid_of(1);
+  const uint32_t grid = grid_of(2), grid_ext = grid_of(1), grid_step = grid_of(3);
+  // Fused engine (default; RTW_WF_FUSED=0: separate extend and shade kernels):
+  // one kernel per bounce, the closest hit computed where the ray is made.
+  const char* fz = getenv("RTW_WF_FUSED");
+  const bool fused = !(fz && *fz == '0');
   // generate -> queue A
   a.out = qa;
   a.seg_out = seg_a;
-  hipError_t e = WfLaunch<R>::gen(a, grid, 0, stream);
+  hipError_t e = fused ? WfLaunch<R>::gen_hit(a, grid_step, lds, stream) : WfLaunch<R>::gen(a, grid, 0, stream);
   if (e != hipSuccess) return fail(RTW_EHIP, "wavefront generate launch: %s", hipGetErrorString(e));
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
@@ -719,9 +739,13 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       a.out = even ? qb : qa;
       a.seg_in = even ? seg_a : seg_b;
       a.seg_out = even ? seg_b : seg_a;
-      if ((e = WfLaunch<R>::ext(a, grid_ext, lds, stream)) != hipSuccess ||
-          (e = WfLaunch<R>::shd(a, grid, lds, stream, stats)) != hipSuccess)
+      if (fused) {
+        if ((e = WfLaunch<R>::step(a, grid_step, lds, stream, stats)) != hipSuccess)
+          st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
+      } else if ((e = WfLaunch<R>::ext(a, grid_ext, lds, stream)) != hipSuccess ||
+                 (e = WfLaunch<R>::shd(a, grid, lds, stream, stats)) != hipSuccess) {
         st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
+      }
     }
     if (st == RTW_OK && (rtwk::launch_wf_count(seg_a, segs, a.live, stream) != hipSuccess ||
                          hipMemcpyAsync(&poll[batch & 1], a.live, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||

@@ -144,6 +144,8 @@ struct PathBuf {
   uint64_t* rs;
   uint32_t* slot;  // home slot
   uint32_t* dsk;   // depth | (skip + 1) << 16
+  R* ht;           // fused engine: root of the path's closest hit (computed where the ray was made)
+  int32_t* hk;     // fused engine: its table position, -1 = miss
 };
 // Moving bytes per path (one PathBuf entry).
 template <typename R>
@@ -180,6 +182,12 @@ hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t grid, size_t ld
 int wf_blocks_per_cu(int precision, int kernel, size_t lds);
 // live = sum of seg_in[0..n_segs) (one workgroup).
 hipError_t launch_wf_count(const uint32_t* seg_in, uint32_t n_segs, uint32_t* live, hipStream_t s);
+// Fused engine (default): generate + the first closest hit, then one kernel
+// per bounce (shade + the next closest hit; the hit travels with the path).
+hipError_t launch_wf_generate_hit_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_generate_hit_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s);
+hipError_t launch_wf_step_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_wf_step_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 // *bad = violations of the drained state (non-empty segment, unit left in a
 // reservoir, queue head below total_units); 0 after a complete frame.
 hipError_t launch_wf_check_drained(const uint32_t* seg_in, const uint32_t* resv, uint32_t n_segs, const uint32_t* head,

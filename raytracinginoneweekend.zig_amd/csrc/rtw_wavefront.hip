@@ -147,6 +147,20 @@ __device__ __forceinline__ void push_path(const PathBuf<R>& out, uint32_t seg_ba
   out_n += (uint32_t)__popcll(m);
 }
 
+// The same with the path's closest hit (fused engine).
+template <typename R>
+__device__ __forceinline__ void push_path_hit(const PathBuf<R>& out, uint32_t seg_base, uint32_t& out_n, bool live,
+                                              const Lane<R>& L, uint32_t slot, int hit, R tmax) {
+  const uint64_t m = __ballot(live);
+  if (live) {
+    const uint32_t i = seg_base + out_n + mbcnt64(m);
+    store_path(out, i, L, slot);
+    out.ht[i] = tmax;
+    out.hk[i] = hit;
+  }
+  out_n += (uint32_t)__popcll(m);
+}
+
 template <typename R>
 __device__ __forceinline__ uint32_t chunk_end(const TraceArgs<R>& A, uint32_t c) {
   return min(c * A.chunk + A.chunk, A.spp);
@@ -253,11 +267,22 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
   return valid && (!ended || need_sample);
 }
 
+#ifndef RTW_WF_EXT_OCC
+#define RTW_WF_EXT_OCC 5  // 6 measured 4 % faster per launch but spills 44 B/lane (wf_extend PMC traffic 104 vs 60 GB/frame)
+#endif
+constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
+template <typename R>
+constexpr int kWfExtendVar = sizeof(R) == 8 ? kVarFastSqrt : 0;
 // ---------------------------------------------------------------- generate --
 // Every slot of the wave's segments takes a unit and starts its first sample.
-template <typename R, bool F32>
+// HIT (fused engine): also the first closest hit of every new path.
+template <typename R, bool F32, bool HIT>
 __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
   const uint32_t lid = lane_id();
+  LdsTables<R> T{};
+  if constexpr (HIT) T = stage_tables<R>(A.t.sc, lds_raw);
+  KStats st;
   for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
     const uint32_t base = seg * kSegCap;
     uint32_t qnext = 0, qend = 0, out_n = 0;
@@ -275,7 +300,14 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
         A.home_sum[3 * (size_t)slot] = A.home_sum[3 * (size_t)slot + 1] = A.home_sum[3 * (size_t)slot + 2] = 0.0;
         start_path(A.t, unit, s, L);
       }
-      push_path(A.out, base, out_n, got, L, slot);
+      if constexpr (HIT) {
+        int hit = -1;
+        R tmax = (R)__builtin_huge_val();
+        if (got) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, hit, tmax);
+        push_path_hit(A.out, base, out_n, got, L, slot, hit, tmax);
+      } else {
+        push_path(A.out, base, out_n, got, L, slot);
+      }
     }
     if (lid == 0) {
       A.seg_out[seg] = out_n;
@@ -291,12 +323,6 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
 // would sit in SGPRs for the whole kernel, at the 100-SGPR limit), the exact
 // fast f64 sqrt (kVarFastSqrt), and a waves-per-SIMD target for the register
 // allocator (kWfExtendOcc, chosen by A/B on MI355X).
-#ifndef RTW_WF_EXT_OCC
-#define RTW_WF_EXT_OCC 5  // 6 measured 4 % faster per launch but spills 44 B/lane (wf_extend PMC traffic 104 vs 60 GB/frame)
-#endif
-constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
-template <typename R>
-constexpr int kWfExtendVar = sizeof(R) == 8 ? kVarFastSqrt : 0;
 template <typename R, bool F32>
 __global__ void __launch_bounds__(kTraceBlock, kWfExtendOcc) wf_extend(WfArgs<R> A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -386,6 +412,60 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
     A.seg_resv[2 * seg] = qnext;
     A.seg_resv[2 * seg + 1] = qend;
   }
+  }
+}
+
+// -------------------------------------------------------- step (fused) --
+// The fused engine's bounce kernel: shade_step on the path's stored hit, then
+// the closest hit of the lane's next ray (the bounced ray or the next
+// sample's camera ray) in registers; live paths are appended to the output
+// queue WITH their hit, so no separate extend launch re-reads the rays.
+// Per bounce segment: path + hit read (108 B f64), path + hit written.
+#ifndef RTW_WF_STEP_OCC
+#define RTW_WF_STEP_OCC 4
+#endif
+template <typename R, bool F32, bool STATS>
+__global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R> A) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const uint32_t lid = lane_id();
+  if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
+    if (lid == 0)
+      for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) A.seg_out[seg] = 0u;
+    return;
+  }
+  const LdsTables<R> T = stage_tables<R>(A.t.sc, lds_raw);
+  KStats st;
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+    const uint32_t n_in = A.seg_in[seg];
+    if (n_in == 0u) {
+      if (lid == 0) A.seg_out[seg] = 0u;
+      continue;
+    }
+    const uint32_t base = seg * kSegCap;
+    uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
+    static_assert(kSegCap == 64, "one path per lane per segment");
+    const uint32_t i = base + lid;
+    const bool valid = lid < n_in;
+    Lane<R> L{};
+    L.skip = -1;
+    uint32_t slot = 0;
+    int hit = -1;
+    R tmax = (R)0;
+    if (valid) {
+      load_path(A.in, i, L, slot);
+      hit = A.in.hk[i];
+      tmax = A.in.ht[i];
+    }
+    const bool live = shade_step<R, F32, STATS>(A, T, lid, valid, L, slot, hit, tmax, qnext, qend);
+    int nh = -1;
+    R nt = (R)__builtin_huge_val();
+    if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
+    push_path_hit(A.out, base, out_n, live, L, slot, nh, nt);
+    if (lid == 0) {
+      A.seg_out[seg] = out_n;
+      A.seg_resv[2 * seg] = qnext;
+      A.seg_resv[2 * seg + 1] = qend;
+    }
   }
 }
 
@@ -479,7 +559,13 @@ hipError_t launch_wf_count(const uint32_t* seg, uint32_t n, uint32_t* live, hipS
 template <typename R, bool F32>
 static hipError_t launch3(int k, const WfArgs<R>& a, uint32_t grid, size_t lds, hipStream_t s) {
   if (k == 0)
-    hipLaunchKernelGGL((wf_generate<R, F32>), dim3(grid), dim3(kTraceBlock), 0, s, a);
+    hipLaunchKernelGGL((wf_generate<R, F32, false>), dim3(grid), dim3(kTraceBlock), 0, s, a);
+  else if (k == 6)
+    hipLaunchKernelGGL((wf_generate<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 7)
+    hipLaunchKernelGGL((wf_step<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 8)
+    hipLaunchKernelGGL((wf_step<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (k == 1)
     hipLaunchKernelGGL((wf_extend<R, F32>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (k == 2)
@@ -507,6 +593,18 @@ hipError_t launch_wf_finish_f64(const WfArgs<double>& a, uint32_t g, size_t l, h
 hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
   return launch3<float, true>(stats ? 5 : 4, a, g, l, s);
 }
+hipError_t launch_wf_generate_hit_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
+  return launch3<double, false>(6, a, g, l, s);
+}
+hipError_t launch_wf_generate_hit_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
+  return launch3<float, true>(6, a, g, l, s);
+}
+hipError_t launch_wf_step_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<double, false>(stats ? 8 : 7, a, g, l, s);
+}
+hipError_t launch_wf_step_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<float, true>(stats ? 8 : 7, a, g, l, s);
+}
 hipError_t launch_wf_generate_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<float, true>(0, a, g, l, s);
 }
@@ -520,9 +618,10 @@ hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t g, size_t l, hip
 template <typename R, bool F32>
 static int occ_wf(int kernel, size_t lds) {
   int n = 0;
-  const hipError_t e = kernel == 1
-                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_extend<R, F32>, kTraceBlock, lds)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shade<R, F32, false>, kTraceBlock, lds);
+  const hipError_t e =
+      kernel == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_extend<R, F32>, kTraceBlock, lds)
+      : kernel == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_step<R, F32, false>, kTraceBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shade<R, F32, false>, kTraceBlock, lds);
   return (e == hipSuccess && n > 0) ? n : 1;
 }
 int wf_blocks_per_cu(int precision, int kernel, size_t lds) {

@@ -1,6 +1,7 @@
 """GPU parity of the wavefront engine (BASELINE.json configs[3]: SoA path
-queues in HBM, per-bounce extend/shade kernels, persistent grids, and the
-in-register drain wf_finish once slots retire).
+queues in HBM, per-bounce kernels — fused shade + closest hit, or separate
+extend / shade — persistent grids, and the in-register drain wf_finish once
+slots retire).
 
 It computes the same Tier-B image as the megakernel: every sample runs the
 same device functions in the same order and a home slot adds its unit's
@@ -21,9 +22,18 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True, params=["finish", "queues"])
 def drain(request, monkeypatch):
     """Every test runs with both drains: wf_finish in registers once slots
-    retire (the default) and the (extend, shade) queues to the end
+    retire (the default) and the bounce kernels' queues to the end
     (RTW_WF_FINISH=0, read by the library on every render)."""
     monkeypatch.setenv("RTW_WF_FINISH", "1" if request.param == "finish" else "0")
+    return request.param
+
+
+@pytest.fixture(autouse=True, params=["fused", "split"])
+def engine_form(request, monkeypatch):
+    """... and both forms of the engine: one fused kernel per bounce (shade +
+    the next closest hit, the default) and separate extend / shade kernels
+    (RTW_WF_FUSED=0)."""
+    monkeypatch.setenv("RTW_WF_FUSED", "1" if request.param == "fused" else "0")
     return request.param
 
 
