@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
 // queue WITH their hit, so no separate extend launch re-reads the rays.
 // Per bounce segment: path + hit read (108 B f64), path + hit written.
 #ifndef RTW_WF_STEP_OCC
-#define RTW_WF_STEP_OCC 4
+#define RTW_WF_STEP_OCC 5  // profiles/r02/wf_step_ab.txt: 5 waves (32-B spill) ~3 % faster than 4
 #endif
 template <typename R, bool F32, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R> A) {
