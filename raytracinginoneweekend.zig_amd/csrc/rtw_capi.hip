@@ -821,6 +821,7 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
     } else {
       rtwk::TraceArgs<double> a;
       fill_args(a, sc->v64, cam, p, ws, L);
+      a.sc.cluster_on = clusters_usable(sc, cam);
       st = run_wavefront<double>(a, p, ws, L, dev, lds, stream, mode == 1);
     }
     if (st != RTW_OK) return st;
