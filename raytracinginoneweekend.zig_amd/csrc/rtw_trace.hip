@@ -167,10 +167,13 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     }
   };
   // One closest-hit step for a lane with a live ray (main.zig:103-112).
-  auto bounce = [&](bool& ended, bool& shading, uint32_t& kind, int& hit, R& tmax) {
+  // Returns 1 when the sample ended (depth limit or miss), 2 when the hit is
+  // to be shaded.  (A result code, not two bool& outputs: the optimiser merged
+  // their stores through a selected pointer, which put both flags in scratch
+  // memory — a store + load per iteration on the critical path.)
+  auto bounce = [&](uint32_t& kind, int& hit, R& tmax) -> int {
     if (L.depth == RTW_KA(max_depth)) {  // rayColor depth == 0 (main.zig:105-108)
-      ended = true;
-      return;
+      return 1;
     }
     if (STATS) st.segments++;
     if constexpr (STATS) {
@@ -186,11 +189,10 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       L.sx += (double)col.x;
       L.sy += (double)col.y;
       L.sz += (double)col.z;
-      ended = true;
-    } else {
-      kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
-      shading = true;
+      return 1;
     }
+    kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
+    return 2;
   };
 
   if constexpr ((VAR & kVarMergedStart) != 0) {
@@ -234,7 +236,11 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       hit = -1;
       tmax = kInf;
       bool ended = false;
-      if (have_ray) bounce(ended, shading, kind, hit, tmax);
+      if (have_ray) {
+        const int b = bounce(kind, hit, tmax);
+        ended = b == 1;
+        shading = b == 2;
+      }
       RTW_STAMP(3)
       if (ended) finish_sample();
     }
@@ -289,7 +295,11 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     uint32_t kind = 0;
     int hit = -1;
     R tmax = kInf;
-    if (have_ray) bounce(ended, shading, kind, hit, tmax);
+    if (have_ray) {
+      const int b = bounce(kind, hit, tmax);
+      ended = b == 1;
+      shading = b == 2;
+    }
     RTW_STAMP(3)
     {
       // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.

@@ -271,9 +271,9 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
 #define RTW_WF_EXT_OCC 5  // 6 measured 4 % faster per launch but spills 44 B/lane (wf_extend PMC traffic 104 vs 60 GB/frame)
 #endif
 constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
-template <typename R>
 // (The clustered pretest, +5 % in the megakernel, made the fused engine 12 % slower:
 // profiles/r02/wf_cluster_ab.txt — its extra registers spill in wf_step.)
+template <typename R>
 constexpr int kWfExtendVar = sizeof(R) == 8 ? kVarFastSqrt : 0;
 // ---------------------------------------------------------------- generate --
 // Every slot of the wave's segments takes a unit and starts its first sample.
