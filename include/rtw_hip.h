@@ -81,7 +81,9 @@ typedef enum {
 /* Render engine (both compute the same Tier-B image, bit for bit). */
 typedef enum {
   RTW_ENGINE_MEGAKERNEL = 0,  /* one persistent trace kernel (BASELINE.json configs[1]) */
-  RTW_ENGINE_WAVEFRONT = 1    /* per-bounce kernels over SoA path queues in HBM (configs[3]) */
+  RTW_ENGINE_WAVEFRONT = 1    /* per-bounce kernels over SoA path queues in HBM (configs[3]): one fused
+                                 shade + closest-hit kernel per bounce (env RTW_WF_FUSED=0: separate
+                                 extend / shade kernels; same image) */
 } rtw_engine;
 
 typedef struct {
@@ -164,7 +166,7 @@ int rtw_render_device(rtw_scene scene, const rtw_camera *cam, const rtw_params *
 /* Statistics pass (diagnostic, not the product path's timing): counts the
  * bounce segments and sphere tests the same render performs.  counts_out[4] =
  * {samples, segments, static_tests, moving_tests}. Synchronous.  Both engines
- * count samples and segments (the wavefront engine in its shade kernel). */
+ * count samples and segments (the wavefront engine in its shading step). */
 int rtw_render_counts(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                       void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
 /* The same pass with counts_out[6]: the four above, then the segments traced
