@@ -163,8 +163,8 @@ __device__ __forceinline__ bool root_obj(const PrimRec& q, const RaySp& s, D tim
   if (kind == 3u) return rect_root(r, o.y, o.x, o.z, d.y, d.x, d.z, tmin, t);
   return rect_root(r, o.x, o.y, o.z, d.x, d.y, d.z, tmin, t);
 }
-template <int FEAT>
-__device__ __forceinline__ bool prim_root(const WorldView& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
+template <int FEAT, typename WV>
+__device__ __forceinline__ bool prim_root(const WV& W, const PrimRec& q, V o, V d, D time, D tmin, D& t) {
   const int xf = (int)(q.meta0 >> 8) - 1;
   if ((FEAT & kFeatXform) && xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
   RaySp s;
@@ -198,8 +198,8 @@ __device__ __forceinline__ void accept(WHit& h, D t, int pos, int orig, D tmin) 
 
 // The reference's literal sequential loop (HittableList.hit, :231-244) over
 // the list in its original order; `order` maps list index -> stored position.
-template <int FEAT>
-__device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* order, V o, V d, D time, D tmin,
+template <int FEAT, typename WV>
+__device__ __forceinline__ void seq_hit(const WV& W, const uint32_t* order, V o, V d, D time, D tmin,
                                         WHit& h) {
   h.pos = -1;
   h.orig = -1;
@@ -215,8 +215,8 @@ __device__ __forceinline__ void seq_hit(const WorldView& W, const uint32_t* orde
   }
 }
 
-template <int MODE, int FEAT>
-__device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack, const V& o, const V& d, D time,
+template <int MODE, int FEAT, typename WV>
+__device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const V& o, const V& d, D time,
                                         D tmin, WHit& h, unsigned long long& nv, unsigned long long& nt) {
   h.pos = -1;
   h.orig = -1;
@@ -347,8 +347,8 @@ __device__ __forceinline__ void closest(const WorldView& W, D m, uint32_t* stack
 }
 
 // Texture.value (texture.zig:36-144) for the winner's record.
-template <int FEAT>
-__device__ __forceinline__ V tex_value(const WorldView& W, uint32_t ti, D u, D v, V p) {
+template <int FEAT, typename WV>
+__device__ __forceinline__ V tex_value(const WV& W, uint32_t ti, D u, D v, V p) {
   const D* t = W.tex + kWorldRec * ti;
   const uint32_t* th = reinterpret_cast<const uint32_t*>(t);
   switch (th[0]) {
@@ -413,7 +413,14 @@ template <int MODE, int OCC, int FEAT>
 __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kBvhStack;  // this wave's stack
-  const WorldView W = A.w;  // a local copy: no reference to the by-value argument escapes
+  // The world's fields are re-read from the kernel argument where used
+  // (scalar loads through a laundered kernarg pointer) instead of living in
+  // SGPRs for the whole kernel: at the 100-SGPR limit they spill to VGPR
+  // lanes (v_writelane / v_readlane in the traversal loop).  As the
+  // megakernel's scene fields (rtw_trace.hip VAR bit 512); +1.4 % on the
+  // globe and Cornell (profiles/r02/world_karg_ab.txt).
+  const RTW_CONST WorldView& W =
+      opaque((const RTW_CONST WorldArgs*)__builtin_amdgcn_kernarg_segment_ptr())->w;
   const D margin = A.margin;
   const uint32_t* order = W.order;
   const uint32_t lid = lane_id();
