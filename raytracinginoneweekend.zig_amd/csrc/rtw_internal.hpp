@@ -112,10 +112,12 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 // profiles/r01/ab_defaults.txt): scalar sphere records + 512 (scene fields from
 // the kernel argument) + kVarR0Table + kVarMergedStart + kVarPreDraw; f64 also
 // 4 waves/SIMD (4) + kVarFastSqrt + kVarCluster (round 2, +5.4 %,
-// profiles/r02/cluster_ab.txt), f32 5 waves/SIMD (8).  Every other variant
+// profiles/r02/cluster_ab.txt) + 1024 (the loop's argument fields re-read from
+// the kernel argument too: +0.6 %, profiles/r02/var1024_ab.txt), f32 5
+// waves/SIMD (8).  Every other variant
 // exists only in the -DRTW_MEASURE build.
 #ifndef RTW_DEFAULT_VAR_F64  // (A/B builds override it)
-#define RTW_DEFAULT_VAR_F64 (4 + 512 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3047940 (+ kVarCluster)
+#define RTW_DEFAULT_VAR_F64 (4 + 512 + 1024 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3048964
 #endif
 constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
 constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
