@@ -500,8 +500,8 @@ def main():
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
             "valu_issue": valu_issue(args, W, H, spp),
-            "note": "megakernel is VALU-issue bound (valu_issue.busy_frac: the VALU issues in ~88 % of SIMD "
-                    "cycles; f64, f32 and integer-multiply wave64 instructions each take ~4 cycles) plus "
+            "note": "megakernel is VALU-issue bound (valu_issue.busy_frac: the fraction of SIMD cycles in "
+                    "which the VALU issues; f64, f32 and integer-multiply wave64 instructions each take ~4 cycles) plus "
                     "divergence; `achieved` counts only the algorithm's sphere-test flops; MFMA n/a (no "
                     "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
         }
