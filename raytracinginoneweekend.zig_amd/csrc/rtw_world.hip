@@ -26,6 +26,11 @@
 #include "rtw_device.hpp"
 #include "rtw_libm.hpp"
 
+// BVH stack with its top entry held in a register (A/B switch; same traversal order).
+#ifndef RTW_WORLD_TOPCACHE
+#define RTW_WORLD_TOPCACHE 1
+#endif
+
 namespace rtwk {
 
 using D = double;
@@ -280,6 +285,9 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, W.cull_rho);
   const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(W.cull));
   uint32_t sp = 0, node = 0;  // wave-uniform
+#if RTW_WORLD_TOPCACHE
+  uint32_t top = 0;  // the stack's top entry (valid while sp > 0); stack[0 .. sp-1] hold the ones below it
+#endif
   auto leaf = [&](uint32_t ref) {
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & kLeafCountMask;
     bool need0 = true, need1 = true;
@@ -333,7 +341,12 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       const uint32_t v0 = (uint32_t)__popcll(__ballot(hit[0] && (!hit[1] || tn[0] <= tn[1])));
       const uint32_t v1 = (uint32_t)__popcll(__ballot(hit[1] && (!hit[0] || tn[1] < tn[0])));
       const bool first0 = v0 >= v1;
+#if RTW_WORLD_TOPCACHE
+      stack[sp++] = top;  // (entry 0 is a dummy when the stack was empty)
+      top = first0 ? r1 : r0;
+#else
       stack[sp++] = first0 ? r1 : r0;
+#endif
       node = first0 ? r0 : r1;
     } else if (i0) {
       node = r0;
@@ -341,7 +354,14 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       node = r1;
     } else {
       if (sp == 0) break;
+#if RTW_WORLD_TOPCACHE
+      // The top entry lives in a register: the pop waits on no LDS read; the
+      // next top's LDS read is issued now and overlaps this node's loads.
+      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)top);
+      top = stack[--sp];
+#else
       node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);  // uniform: scalar loads
+#endif
     }
   }
 }
