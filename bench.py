@@ -264,7 +264,7 @@ def wavefront_bytes(counts, precision, units):
 
 
 def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, samples_all, world, rank, dist,
-                      gather_image, torch):
+                      tg, torch):
     """configs[3]: the same frame on the wavefront engine (bit-identical image,
     tests/test_gpu_wavefront.py), timed the same way; roofline = HBM (the
     path queues stream through HBM every bounce)."""
@@ -281,7 +281,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     for i in range(args.steps):
         rend.render(cam, p, out=out, timer=timers[i])
         if world > 1:
-            gather_image(out, H, rank, world)
+            tg.gather(out)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -347,7 +347,7 @@ def dry_run(args):
     import torch
     import torch.distributed as dist
 
-    from rtw_amd.shard import gather_image, shard_rows
+    from rtw_amd.shard import TileGather, shard_rows
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
@@ -355,18 +355,41 @@ def dry_run(args):
     W, H, spp = workload(args, world)
     rb, rs, rc = shard_rows(H, rank, world)
     out = torch.full((rc, 4, 3), rank, dtype=torch.uint8)
-    img = gather_image(out, H, rank, world)
+    tg = TileGather(out, H, rank, world)
+    t0 = time.perf_counter()
+    for _ in range(max(1, args.steps)):
+        tg.gather(out)
+    step_ms = (time.perf_counter() - t0) / max(1, args.steps) * 1e3
+    img = tg.image()
     samples = torch.tensor([float(rc * W * spp)], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(samples)
+    # the per-rank timing fields of the GPU line (the "trace" here is the dry step)
+    per = rank_times(dist, world, step_ms, step_ms, torch.device("cpu"))
     if rank == 0:
         ok = bool((img[:, 0, 0] == torch.arange(H) % world).all())
         print(json.dumps({"dry_run": True, "dist": {"backend": dist.get_backend() if world > 1 else None,
-                                                    "world_size": world},
+                                                    "world_size": world, **per},
                           "width": W, "height": H, "spp_frame": spp, "samples_all": samples.item(),
                           "rows_interleaved_ok": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rank_times(dist, world, step_ms, trace_ms, dev):
+    """Every rank's mean step time and mean trace-kernel time (all_gather) and
+    the trace imbalance max/mean: whether the interleaved rows balance."""
+    import torch
+    mine = torch.tensor([step_ms, trace_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        allr = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    step = [round(float(x[0]), 3) for x in allr]
+    trace = [round(float(x[1]), 3) for x in allr]
+    return {"rank_step_ms": step, "rank_trace_ms": trace,
+            "imbalance": round(max(trace) / (sum(trace) / len(trace)), 4) if sum(trace) > 0 else None}
 
 
 def workload(args, world):
@@ -392,7 +415,7 @@ def main():
 
     import rtw_amd as R
     from rtw_amd.device import TorchRenderer
-    from rtw_amd.shard import gather_image, shard_rows
+    from rtw_amd.shard import TileGather, shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -422,6 +445,7 @@ def main():
     rend = TorchRenderer(sph, mats, local)
     out = torch.empty((rc, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
     samples_rank = rc * W * spp
+    tg = TileGather(out, H, rank, world)  # send tile + rank 0's receive tiles, allocated once
 
     # Untimed: counts pass (algorithmic flops of one trace launch) + warmup.
     counts = rend.counts(cam, R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
@@ -429,7 +453,7 @@ def main():
     for _ in range(args.warmup):
         rend.render(cam, params, out=out)
         if world > 1:
-            gather_image(out, H, rank, world)
+            tg.gather(out)
     torch.cuda.synchronize()
 
     # One HIP-event pair per step brackets that step's trace-kernel launch on
@@ -442,7 +466,7 @@ def main():
     for i in range(args.steps):
         rend.render(cam, params, out=out, timer=timers[i])
         if world > 1:
-            gather_image(out, H, rank, world)
+            tg.gather(out)  # RCCL gather of the row tile to rank 0 (no allocation, no assembly)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -454,7 +478,11 @@ def main():
         t.close()
 
     dist_info = {"backend": None, "world_size": 1, "samples_per_rank": [samples_rank], "gather_ms": None}
+    per_rank_t = rank_times(dist, world, elapsed / args.steps * 1e3, trace_ms_avg, torch.device("cuda", local))
     if world > 1:
+        frame = tg.image()  # rank 0 interleaves the last gathered tiles once, after the timed region
+        if rank == 0:
+            assert frame.shape == (H, W, 3)
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -466,13 +494,14 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        gather_image(out, H, rank, world)
+        tg.gather(out)
         torch.cuda.synchronize()
         gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                      "samples_per_rank": per_rank, "gather_ms": round(float(gt.item()) * 1e3, 3)}
-    else:
+    dist_info.update(per_rank_t)
+    if world == 1:
         samples_all = float(samples_rank)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -529,7 +558,7 @@ def main():
         for _ in range(args.steps):
             rend.render(cam, p32, out=out)
             if world > 1:
-                gather_image(out, H, rank, world)
+                tg.gather(out)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -545,7 +574,7 @@ def main():
 
     if not args.no_wavefront_variant and args.engine == "megakernel":
         extra["wavefront_variant"] = wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts,
-                                                       samples_all, world, rank, dist, gather_image, torch)
+                                                       samples_all, world, rank, dist, tg, torch)
 
     if world == 1 and not args.no_world_variants:
         extra["globe_10k_variant"] = world_variant(R, torch, 7, max(2, args.steps // 2), 1)

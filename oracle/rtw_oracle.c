@@ -325,7 +325,7 @@ typedef struct {
   V3 bg;
   uint64_t *rng;
   ro_stats st;
-  uint32_t flags; /* RO_BOOK1_* (ro_render_tier_a_ex), 0 = the current main.zig */
+  uint32_t flags; /* RO_BOOK1_* / RO_MUT_* (ro_render_tier_a_ex), 0 = the current main.zig */
 } CtxA;
 
 /* MovingSphere.center, hittable.zig:219-221 */
@@ -410,13 +410,22 @@ static inline double reflectance(double cosine, double ref_idx) {
   return r1 + (1.0 - r1) * zig_pow_posint(1.0 - cosine, 5.0);
 }
 
+/* reflectance with another Schlick exponent: test control only (RO_MUT_SCHLICK_EXP) */
+static inline double reflectance_exp(double cosine, double ref_idx, double e) {
+  const double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+  const double r1 = r0 * r0;
+  return r1 + (1.0 - r1) * pow(1.0 - cosine, e);
+}
+
 /* Material.scatter (material.zig:22-29) */
 static int scatter_a(CtxA *cx, const RayA *r_in, const HitA *rec, V3 *att, RayA *scattered) {
   const ro_material *m = &cx->scene->mats[rec->mat];
   switch (m->kind) {
     case RO_LAMBERT_SOLID:
     case RO_LAMBERT_CHECKER: { /* material.zig:44-52 */
-      V3 dir = vadd(rec->normal, vnormalized(rand_in_unit_sphere(cx->rng, &cx->st.draws)));
+      const V3 b = rand_in_unit_sphere(cx->rng, &cx->st.draws);
+      /* RO_MUT_LAMBERT_NONORM: test control only (tests/test_readme_image.py) */
+      V3 dir = vadd(rec->normal, (cx->flags & RO_MUT_LAMBERT_NONORM) ? b : vnormalized(b));
       if (vnear_zero(dir)) dir = rec->normal;
       scattered->origin = rec->p;
       scattered->dir = dir;
@@ -430,6 +439,7 @@ static int scatter_a(CtxA *cx, const RayA *r_in, const HitA *rec, V3 *att, RayA 
       scattered->dir = vadd(reflected, vmul(rand_in_unit_sphere(cx->rng, &cx->st.draws), m->fuzz));
       scattered->time = r_in->time;
       *att = vload(m->albedo);
+      if (cx->flags & RO_MUT_METAL_SCATTERED) return vdot(scattered->dir, rec->normal) > 0.0; /* test control */
       return vdot(reflected, rec->normal) > 0.0;
     }
     case RO_DIELECTRIC: { /* material.zig:72-85 */
@@ -439,9 +449,15 @@ static int scatter_a(CtxA *cx, const RayA *r_in, const HitA *rec, V3 *att, RayA 
       const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
       const int can_refract = ratio * sin_theta <= 1.0;
       int do_refract = 0;
-      if (can_refract) { /* short-circuit `and`: the draw happens only here */
+      if (cx->flags & RO_MUT_DIEL_ALWAYS_DRAW) { /* test control: no short circuit (draws on TIR too) */
         cx->st.draws++;
-        do_refract = reflectance(cos_theta, ratio) < rand01(cx->rng);
+        const double r = rand01(cx->rng);
+        do_refract = can_refract && reflectance(cos_theta, ratio) < r;
+      } else if (can_refract) { /* short-circuit `and`: the draw happens only here */
+        cx->st.draws++;
+        const double refl = (cx->flags & RO_MUT_SCHLICK_EXP) ? reflectance_exp(cos_theta, ratio, 2.0)
+                                                             : reflectance(cos_theta, ratio);
+        do_refract = refl < rand01(cx->rng);
       }
       scattered->origin = rec->p;
       scattered->dir = do_refract ? refract(unit_dir, rec->normal, ratio) : reflect(unit_dir, rec->normal);

@@ -84,7 +84,7 @@ typedef struct {
   uint64_t samples, segments, static_tests, moving_tests, draws;
 } ro_stats;
 
-/* ---- Zig std.Random restatement (Zig 0.14 std/Random/*.zig) ---- */
+/* ---- Zig std.Random restatement (Zig 0.14 std/Random/ *.zig) ---- */
 uint64_t ro_splitmix64_next(uint64_t *state);
 void ro_xoshiro256_seed(uint64_t s[4], uint64_t seed);
 uint64_t ro_xoshiro256_next(uint64_t s[4]);
@@ -112,6 +112,16 @@ uint32_t ro_image_height(uint32_t width, double aspect); /* main.zig:306 */
  * sum_out (optional): W*H*3 f64 per-pixel sums, same layout. */
 #define RO_BOOK1_SKY 1u
 #define RO_BOOK1_NO_TIME 2u
+/* Mutations of one hot-path rule, for the README pin's controls only
+ * (tests/test_readme_image.py measures which of them the pin detects):
+ * Metal absorbs on the scattered direction instead of `reflected`
+ * (material.zig:64); Schlick with exponent 2 instead of 5 (:90); Lambertian
+ * adds the unnormalised in-sphere point (:45); the dielectric draws even
+ * when it cannot refract (no short circuit, :81). */
+#define RO_MUT_METAL_SCATTERED 0x100u
+#define RO_MUT_SCHLICK_EXP 0x200u
+#define RO_MUT_LAMBERT_NONORM 0x400u
+#define RO_MUT_DIEL_ALWAYS_DRAW 0x800u
 void ro_render_tier_a_ex(const ro_scene *scene, const ro_camera *cam, const double bg[3],
                          uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
                          uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats,

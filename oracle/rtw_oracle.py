@@ -230,6 +230,8 @@ def render_tier_a(scene: Scene, cam: Camera, rng: ZigRandom, width: int, height:
 # seeded by SplitMix64, Random.float(f64)), the scene builder's draw order and
 # Tier A's camera / sphere / material arithmetic (tests/test_readme_image.py).
 BOOK1_SKY, BOOK1_NO_TIME = 1, 2  # rtw_oracle.h RO_BOOK1_*
+# rtw_oracle.h RO_MUT_*: one hot-path rule mutated (the pin's controls only)
+MUT_METAL_SCATTERED, MUT_SCHLICK_EXP, MUT_LAMBERT_NONORM, MUT_DIEL_ALWAYS_DRAW = 0x100, 0x200, 0x400, 0x800
 
 
 def readme_scene(seed: int = 42, f64=None):
@@ -280,13 +282,13 @@ def readme_scene(seed: int = 42, f64=None):
     return sc, rng
 
 
-def readme_camera() -> Camera:
+def readme_camera(look_from=(12, 2, 3)) -> Camera:
     """Camera.init (main.zig:52-89) of the README image: 3:2, vfov 20,
     aperture 0.1, focus 10, looking at the origin from (12, 2, 3) — fitted
     to the image (the current scene 1 looks from (13, 2, 3))."""
     cam = Camera()
     arr = C.c_double * 3
-    lib().ro_camera_init(C.byref(cam), arr(12, 2, 3), arr(0, 0, 0), arr(0, 1, 0), 20.0, 1.5, 0.1, 10.0, 0.0, 1.0)
+    lib().ro_camera_init(C.byref(cam), arr(*look_from), arr(0, 0, 0), arr(0, 1, 0), 20.0, 1.5, 0.1, 10.0, 0.0, 1.0)
     return cam
 
 

@@ -520,11 +520,16 @@ void rw_render_tier_b(const rw_world *w, const ro_camera *cam, const ro_params *
   {
     ro_stats st;
     memset(&st, 0, sizeof(st));
+    /* work item = (row, block of 32 pixels): a few rows of a large world
+     * (configs[4]: 10k primitives tested per segment) still use every thread */
+    const uint32_t nblk = (W + 31) / 32;
 #pragma omp for schedule(dynamic, 1)
-    for (int64_t q = 0; q < (int64_t)p->row_count; ++q) {
+    for (int64_t qb = 0; qb < (int64_t)p->row_count * nblk; ++qb) {
+      const int64_t q = qb / nblk;
       const uint32_t y = p->row_begin + (uint32_t)q * p->row_stride;
       const uint32_t j = H - 1 - y;
-      for (uint32_t i = 0; i < W; ++i) {
+      const uint32_t i_end = (uint32_t)(qb % nblk) * 32 + 32 < W ? (uint32_t)(qb % nblk) * 32 + 32 : W;
+      for (uint32_t i = (uint32_t)(qb % nblk) * 32; i < i_end; ++i) {
         const uint64_t pixel = (uint64_t)y * W + i;
         double tx = 0, ty = 0, tz = 0;
         for (uint32_t c0 = 0; c0 < p->spp; c0 += chunk) {

@@ -565,10 +565,13 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
   a.stats = reinterpret_cast<unsigned long long*>(ws + L.stats_off);
 }
 
-size_t lds_bytes(const rtw_scene_s* sc, int prec) {
+// n_clusters: clusters whose slot -> position table (cpos) is staged, 0 unless
+// the launched kernel runs the clustered pretest (f64 megakernel with
+// kVarCluster and clusters_usable): other paths neither read nor stage it.
+size_t lds_bytes(const rtw_scene_s* sc, int prec, uint32_t n_clusters) {
   const size_t r = prec == 1 ? 4 : 8;
   return rtwk::kCoopLdsBytes + r * (8 * ((size_t)sc->n + 1) + (size_t)sc->n + 8 * (size_t)sc->nm + 4 * (size_t)sc->ng) +
-         4 * ((size_t)sc->n + 1 + sc->nm + sc->n + rtwk::kClusterSlots * (size_t)sc->v64.n_clusters) + 16;
+         4 * ((size_t)sc->n + 1 + sc->nm + sc->n + rtwk::kClusterSlots * (size_t)n_clusters) + 16;
 }
 
 // The clustered pretest's bounding spheres hold each moving member over its
@@ -801,11 +804,17 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
     return fail(RTW_EINVAL, "scene lives on device %d but the current device is %d", sc->device, dev);
   auto* ws = static_cast<unsigned char*>(workspace);
   HIP_TRY(hipMemsetAsync(ws + L.counter_off, 0, 512, stream));  // queue head + stats
-  const size_t lds = lds_bytes(sc, (int)p->precision);
-  if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int var = kernel_variant(p->precision);
   if (p->engine != RTW_ENGINE_WAVEFRONT && !rtwk::trace_variant_built((int)p->precision, var))
     return fail(RTW_EINVAL, "RTW_VARIANT=%d: trace kernel variant not built into this library", var);
+  // The clustered pretest runs only in the f64 megakernel variants with
+  // kVarCluster, and only when the shutter lies in every time group.
+  const uint32_t cl_on = (p->engine == RTW_ENGINE_MEGAKERNEL && p->precision == RTW_PRECISION_F64 &&
+                          (var & rtwk::kVarClusterBit) != 0)
+                             ? clusters_usable(sc, cam)
+                             : 0u;
+  const size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
+  if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);
   const int cus = device_cus(dev);
   uint32_t total_units = 0;
@@ -817,11 +826,13 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
     if (p->precision == RTW_PRECISION_F32) {
       rtwk::TraceArgs<float> a;
       fill_args(a, sc->v32, cam, p, ws, L);
+      a.sc.n_clusters = 0u;  // f32: no clustered pretest
       st = run_wavefront<float>(a, p, ws, L, dev, lds, stream, mode == 1);
     } else {
       rtwk::TraceArgs<double> a;
       fill_args(a, sc->v64, cam, p, ws, L);
-      a.sc.cluster_on = clusters_usable(sc, cam);
+      a.sc.cluster_on = 0u;  // the bounce kernels run the flat pretest
+      a.sc.n_clusters = 0u;
       st = run_wavefront<double>(a, p, ws, L, dev, lds, stream, mode == 1);
     }
     if (st != RTW_OK) return st;
@@ -829,6 +840,7 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   } else if (p->precision == RTW_PRECISION_F32) {
     rtwk::TraceArgs<float> a;
     fill_args(a, sc->v32, cam, p, ws, L);
+    a.sc.n_clusters = 0u;  // f32: no clustered pretest
     total_units = a.total_units;
     const uint32_t want = (total_units + 255) / 256;
     const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));
@@ -836,7 +848,8 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   } else {
     rtwk::TraceArgs<double> a;
     fill_args(a, sc->v64, cam, p, ws, L);
-    a.sc.cluster_on = clusters_usable(sc, cam);
+    a.sc.cluster_on = cl_on;
+    if (!cl_on) a.sc.n_clusters = 0u;  // nothing to stage (lds_bytes above)
     total_units = a.total_units;
     const uint32_t want = (total_units + 255) / 256;
     const uint32_t grid = std::max(1u, std::min((uint32_t)(cus * bpc), want));

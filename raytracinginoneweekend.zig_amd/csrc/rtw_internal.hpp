@@ -120,6 +120,7 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 #define RTW_DEFAULT_VAR_F64 (4 + 512 + 1024 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3048964
 #endif
 constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
+constexpr int kVarClusterBit = 2097152;  // rtw_device.hpp kVarCluster (clustered pretest, f64)
 constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
 bool trace_variant_built(int precision, int var);
 constexpr int kTraceBlock = 256;

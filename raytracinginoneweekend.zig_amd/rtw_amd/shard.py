@@ -37,6 +37,34 @@ def assemble(tiles, height: int, world: int) -> torch.Tensor:
     return out
 
 
+class TileGather:
+    """The gather of one rank's row tile to rank 0 with its buffers allocated
+    once (the padded send tile, rank 0's receive tiles): `gather(local)` is
+    just the copy into the tile + one collective, so a timed loop that
+    gathers every frame allocates nothing; `image()` interleaves the last
+    gathered tiles into the frame on rank 0 (once, outside a timed loop)."""
+
+    def __init__(self, like: torch.Tensor, height: int, rank: int, world: int, group=None):
+        self.height, self.rank, self.world, self.group = height, rank, world, group
+        self.dev = like.device
+        host = like.is_cuda and world > 1 and dist.get_backend(group) == "gloo"  # gloo gathers host tensors only
+        tdev = torch.device("cpu") if host else like.device
+        self.tile = torch.zeros((max_rows(height, world),) + tuple(like.shape[1:]), dtype=like.dtype, device=tdev)
+        self.recv = ([torch.empty_like(self.tile) for _ in range(world)] if rank == 0 else None) if world > 1 \
+            else [self.tile]
+
+    def gather(self, local: torch.Tensor) -> None:
+        self.tile[: local.shape[0]].copy_(local, non_blocking=self.tile.device == local.device)
+        if self.world > 1:
+            dist.gather(self.tile, gather_list=self.recv, dst=0, group=self.group)
+
+    def image(self):
+        """The assembled (height, W, C) frame on rank 0, None elsewhere."""
+        if self.rank != 0:
+            return None
+        return assemble(self.recv, self.height, self.world).to(self.dev)
+
+
 def gather_image(local: torch.Tensor, height: int, rank: int, world: int, group=None):
     """Gather every rank's rows to rank 0 and interleave them; None on other ranks."""
     mr = max_rows(height, world)

@@ -32,8 +32,12 @@ def run_bench(*argv, timeout=240):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_plain_invocation_spawns_n_ranks(n):
-    r = run_bench("--gpus", str(n), "--steps", "1", "--warmup", "0")
-    assert r["dist"] == {"backend": "gloo", "world_size": n}
+    r = run_bench("--gpus", str(n), "--steps", "2", "--warmup", "0")
+    d = r["dist"]
+    assert (d["backend"], d["world_size"]) == ("gloo", n)
+    # per-rank timings and the trace imbalance (max / mean) of the GPU line
+    assert len(d["rank_step_ms"]) == len(d["rank_trace_ms"]) == n
+    assert d["imbalance"] >= 1.0 and abs(d["imbalance"] - max(d["rank_trace_ms"]) * n / sum(d["rank_trace_ms"])) < 0.05
     assert r["rows_interleaved_ok"]
     # configs[1] weak scaling: the 1200x675 frame at n x 500 spp
     assert (r["width"], r["height"], r["spp_frame"]) == (1200, 675, 500 * n)

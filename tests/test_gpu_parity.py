@@ -140,6 +140,76 @@ def test_custom_scene_parity(rtw, oracle, precision):
     assert_parity(g, o, f"custom {precision}")
 
 
+def clustered_scene(rtw, n_narrow=101, seed=7):
+    """Many narrow spheres in THREE time groups that all contain the camera
+    shutter [0, 1] ([0, 1], [-0.5, 1.5], [-1, 2]), so the clustered pretest
+    (rtw_capi.hip clusters_usable) is on and its clusters mix
+    groups: static members, movers along x, y and z, and an odd member count
+    in the last cluster (101 narrow spheres = 12 x 8 + 5)."""
+    rng = np.random.default_rng(seed)
+    M = rtw.Material
+    mats = (M * 5)()
+    mats[0].kind = rtw.LAMBERT_CHECKER
+    mats[0].albedo[:] = (0.9, 0.9, 0.9)
+    mats[0].albedo_odd[:] = (0.2, 0.3, 0.1)
+    mats[1].kind = rtw.LAMBERT_SOLID
+    mats[1].albedo[:] = (0.6, 0.3, 0.2)
+    mats[2].kind, mats[2].fuzz = rtw.METAL, 0.2
+    mats[2].albedo[:] = (0.8, 0.8, 0.7)
+    mats[3].kind, mats[3].ir = rtw.DIELECTRIC, 1.5
+    mats[4].kind = rtw.LAMBERT_SOLID
+    mats[4].albedo[:] = (0.2, 0.5, 0.8)
+    groups = [(0.0, 1.0), (-0.5, 1.5), (-1.0, 2.0)]
+    specs = [((0, -1000, 0), (0, -1000, 0), 1000.0, 0.0, 0.0, 0, 0)]
+    for k in range(n_narrow):
+        x, z = -6 + 12 * rng.random(), -6 + 12 * rng.random()
+        r = 0.12 + 0.25 * rng.random()
+        c0 = (x, r, z)
+        kind = k % 4  # 0 static, 1 x mover, 2 y mover, 3 z mover
+        if kind == 0:
+            specs.append((c0, c0, r, 0.0, 0.0, 0, 1 + k % 4))
+            continue
+        dv = [0.0, 0.0, 0.0]
+        dv[kind - 1] = 0.2 + 0.4 * rng.random()
+        t0, t1 = groups[k % 3]
+        specs.append((c0, tuple(c + d for c, d in zip(c0, dv)), r, t0, t1, 1, 1 + k % 4))
+    sph = (rtw.Sphere * len(specs))()
+    for s, (c0, c1, r, t0, t1, mv, m) in zip(sph, specs):
+        s.c0[:], s.c1[:] = c0, c1
+        s.radius, s.t0, s.t1, s.moving, s.mat = r, t0, t1, mv, m
+    return sph, mats
+
+
+def test_clustered_pretest_mixed_time_groups(rtw, oracle, capfd, monkeypatch):
+    """the clustered pretest with pairs whose members sit in
+    different time groups (per-lane time fraction recomputed per group), the
+    (moving, static) remap of a mixed pair, and odd cluster sizes — against
+    oracle Tier B on the device's default f64 kernel; the counts pass proves
+    the clusters were on and skipped work (cluster_wave_skips > 0)."""
+    from rtw_amd.device import TorchRenderer
+    sph, mats = clustered_scene(rtw)
+    cam = rtw.camera_init((13, 2, 3), (0, 0.3, 0), (0, 1, 0), 30.0, ASPECT, 0.1, 10.0, 0.0, 1.0)
+    kw = dict(width=192, height=108, spp=12, chunk=5)
+    g = gpu_render(rtw, cam, sph, mats, **kw)
+    o = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam), **kw)
+    assert_parity(g, o, "clustered, 3 time groups")
+    assert g.std() > 5
+    monkeypatch.setenv("RTW_COUNTS_VERBOSE", "1")
+    R = TorchRenderer(sph, mats, 0)
+    R.counts(cam, rtw.make_params(192, 108, 12, chunk=5))
+    err = capfd.readouterr().err
+    line = [ln for ln in err.splitlines() if "cluster_wave_skips" in ln][-1]
+    f = line.split()
+    tests, skips = int(f[f.index("cluster_wave_tests") + 1]), int(f[f.index("cluster_wave_skips") + 1])
+    print(line)
+    assert tests > 0 and skips > 0, line
+    # a shutter outside one group turns the clusters off (flat pretest): same image as the oracle too
+    cam2 = rtw.camera_init((13, 2, 3), (0, 0.3, 0), (0, 1, 0), 30.0, ASPECT, 0.1, 10.0, 0.0, 1.2)
+    g2 = gpu_render(rtw, cam2, sph, mats, **kw)
+    o2 = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam2), **kw)
+    assert_parity(g2, o2, "clustered scene, shutter [0, 1.2] (clusters off)")
+
+
 def test_tier_c_vs_reference_stream(rtw, oracle, cover):
     """Config 1 shape (400x225, 16:9) at 24 spp vs Tier A (the reference's
     sequential DefaultPrng(42) stream): statistical parity."""

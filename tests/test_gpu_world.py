@@ -70,6 +70,56 @@ def test_world_globe_parity(rtw, oracle, W, earth):
     assert_parity(g, ref, "globe 64x36x2")
 
 
+def test_globe_config4_workload_equals_oracle(rtw, oracle, W, earth):
+    """BASELINE configs[4] at its bench workload: the globe + 10k-sphere frame
+    at 1200x675x100 through the BVH (leaf pretest, outward-rounded f32 slabs:
+    conservative bounds whose failure mode is a rare dropped hit).  16 rows
+    spread over the frame (y = 7, 49, ..., 637; 1.92 M samples) equal the
+    LINEAR oracle's Tier B (committed fixture, tests/golden/make_world_fixtures.py:
+    ~15 CPU-minutes), and 2 more rows through the globe are rendered by the
+    oracle live here (16 threads)."""
+    import os
+    import time
+
+    from conftest import GOLDEN
+    b = built(W, 7, earth)
+    s = b.settings
+    assert (s.width, s.height, s.spp) == (1200, 675, 100)
+    cam = b.camera()
+    t0 = time.time()
+    g = W.render_world(cam, b.desc, params(rtw, b, s.width, s.height, s.spp))
+    t_gpu = time.time() - t0
+    fx = np.load(os.path.join(GOLDEN, "globe_1200x675x100_rows7s42.npz"))
+    rows = fx["rows"]
+    assert len(rows) == 16 and int(fx["samples"]) == 16 * 1200 * 100
+    d = diff_stats(g[rows], fx["rgb"])
+    print(f"globe 1200x675x100 (GPU {t_gpu:.1f} s incl. upload + BVH build) vs fixture rows 7::42:", d)
+    assert_parity(g[rows], fx["rgb"], "globe configs[4] rows 7::42")
+    o = oracle.OracleWorld(7, 42, image=earth)
+    t0 = time.time()
+    live, st = o.render_tier_b(o.camera(), 1200, 675, 100, row_begin=322, row_stride=42, row_count=2, threads=16)
+    print(f"globe rows 322, 364 live oracle: {time.time() - t0:.1f} s, {st['segments']} segments")
+    assert_parity(g[322:365:42], live, "globe configs[4] rows 322, 364 (live oracle)")
+
+
+def test_cornell_full_frame_equals_oracle(rtw, oracle, W, earth):
+    """The reference's default scene (scene 6, main.zig:259-293, :352-362) at
+    its own settings, 600x600x200 (72 M samples, ~6.6 segments each), the
+    WHOLE frame against oracle world Tier B (16 threads)."""
+    import time
+    b = built(W, 6, earth)
+    s = b.settings
+    assert (s.width, s.height, s.spp) == (600, 600, 200)
+    g = W.render_world(b.camera(), b.desc, params(rtw, b, s.width, s.height, s.spp))
+    o = oracle.OracleWorld(6, 42)
+    t0 = time.time()
+    ref, st = o.render_tier_b(o.camera(), 600, 600, 200, threads=16)
+    print(f"cornell 600x600x200 oracle: {time.time() - t0:.1f} s, {st['segments']} segments")
+    assert st["samples"] == 600 * 600 * 200
+    assert_parity(g, ref, "cornell full frame 600x600x200")
+    assert g.std() > 5
+
+
 def _render_dev(rtw, W, b, cam, p, linear):
     import torch
     dw = W.DeviceWorld(b.desc, linear=linear)

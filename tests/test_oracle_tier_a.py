@@ -67,3 +67,20 @@ def test_tier_a_workload_profile(oracle):
     seg = st["segments"] / st["samples"]
     assert 2.1 < seg < 2.45
     assert 11.0 < st["draws"] / st["samples"] < 13.5
+
+
+def test_config0_artifact(oracle):
+    """BASELINE configs[0] (400x225x100, the Zig CPU reference to PPM) as the
+    oracle's Tier A restatement of the whole main(): the committed digest
+    (tests/golden/make_config0.py) is reproduced bit for bit (~3-10 s, 1 core)."""
+    import hashlib
+    import json
+    import os
+
+    from conftest import GOLDEN
+    rec = json.load(open(os.path.join(GOLDEN, "config0_tier_a_400x225x100.json")))
+    img, st = oracle.main_cover(400, 16 / 9, 100, 50, 42)
+    assert img.shape == (225, 400, 3) and st["samples"] == 400 * 225 * 100 == rec["samples"]
+    ppm = b"P6\n400 225\n255\n" + img.tobytes()
+    assert hashlib.sha256(ppm).hexdigest() == rec["ppm_sha256"]
+    assert [round(float(x), 4) for x in img.reshape(-1, 3).mean(0)] == rec["mean_rgb"]

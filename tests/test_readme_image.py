@@ -95,3 +95,40 @@ def test_float_conversion_is_pinned(ref, renders):
     mf = np.abs(f - ref).mean()
     print(f"mean|d| vs reference image: Zig float {np.abs(a - ref).mean():.2f}, 53-bit fraction {mf:.2f}")
     assert mf > 3.0 * np.abs(a - ref).mean()
+
+
+# Mutation controls: the same scene rendered with ONE
+# hot-path rule changed (oracle/rtw_oracle.h RO_MUT_*), to measure what the
+# pin can see.  The statistic is deterministic (the seed-42 stream); across
+# independent render streams of the unmutated oracle it varies by < 0.05
+# (7.12-7.18 on 6 streams), so a rule counts as pinned when it moves mean|d|
+# against the reference image by more than REJECT above the oracle's value.
+REJECT = 0.25
+MUTATIONS = {  # name: (flags, look_from, pinned by the README image?)
+    "lambert_unnormalised (material.zig:45)": (O.MUT_LAMBERT_NONORM, (12, 2, 3), True),
+    "schlick_exponent_2 (material.zig:90)": (O.MUT_SCHLICK_EXP, (12, 2, 3), True),
+    "camera_from_13_2_3 (unfitted, main.zig:320)": (0, (13, 2, 3), True),
+    "camera_from_12.5_2_3": (0, (12.5, 2, 3), True),
+    "metal_absorbs_on_scattered (material.zig:64)": (O.MUT_METAL_SCATTERED, (12, 2, 3), False),
+    "dielectric_draws_without_short_circuit (material.zig:81)": (O.MUT_DIEL_ALWAYS_DRAW, (12, 2, 3), False),
+}
+
+
+def test_mutation_controls(ref, renders):
+    """Which hot-path rules the README pin detects: a wrong Lambertian
+    normalisation, Schlick exponent or camera position moves the image
+    measurably away from the reference's; Metal's absorption test on the
+    scattered instead of the reflected direction, and a dielectric draw
+    without the short circuit (a stream shift only), do not — those rules are
+    pinned only by the two self-restatements (C and Python)."""
+    base = np.abs(renders["42"][0] - ref).mean()
+    got = {}
+    for name, (flags, look_from, pinned) in MUTATIONS.items():
+        sc, rng = O.readme_scene(42)
+        img, _ = O.render_tier_a_ex(sc, O.readme_camera(look_from), rng, W, H, SPP,
+                                    flags=O.BOOK1_SKY | O.BOOK1_NO_TIME | flags)
+        got[name] = np.abs(img.astype(np.float64) - ref).mean()
+        print(f"{name:58s} mean|d| {got[name]:6.3f} (oracle {base:.3f}): "
+              f"{'REJECTED' if got[name] > base + REJECT else 'not detected'}")
+    for name, (_, _, pinned) in MUTATIONS.items():
+        assert (got[name] > base + REJECT) == pinned, (name, got[name], base)

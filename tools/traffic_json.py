@@ -1,5 +1,5 @@
 """Per-launch HBM traffic of the f64 trace kernel from the FETCH_SIZE / WRITE_SIZE
-PMC passes (tools/gpu_bench_profile.sh) -> profiles/<tag>/traffic.json, read by
+PMC passes (tools/gpu_evidence.sh, stage pmc) -> profiles/<tag>/traffic.json, read by
 bench.py for roofline.traffic.  FETCH_SIZE is doubled (gfx950 tallies 128-B
 reads at 64 B, MI355X_MICROARCH.md §HBM); units are KB (rocprofv3)."""
 import csv
