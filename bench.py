@@ -75,14 +75,17 @@ def parse():
     return parse_args()
 
 
+EVIDENCE_ROUNDS = ("r03", "r02", "r01")  # newest first
+
+
 def evidence(name):
-    """Path of a committed PMC evidence file: this round's (profiles/r02)
-    when present, else round 1's."""
-    for rnd in ("r02", "r01"):
+    """Path of a committed PMC evidence file: the newest round's copy
+    (profiles/r03, else r02, else r01)."""
+    for rnd in EVIDENCE_ROUNDS:
         path = os.path.join(REPO, "profiles", rnd, name)
         if os.path.exists(path):
             return path
-    return os.path.join(REPO, "profiles", "r01", name)
+    return os.path.join(REPO, "profiles", EVIDENCE_ROUNDS[-1], name)
 
 
 def traffic_per_launch(args, W, H, spp):
@@ -172,10 +175,10 @@ def world_roofline(scene, s, kernel_ms, info):
     scalar loads (no per-lane byte stream to price against HBM), so the roof
     is the SIMDs' instruction issue: 1024 SIMDs x clock / 4 cycles per wave64
     VALU instruction.  achieved = the VALU instructions of one launch (PMC
-    SQ_INSTS_VALU of the same config, profiles/r02/world_pmc_<scene>.json,
+    SQ_INSTS_VALU of the same config, profiles/rNN/world_pmc_<scene>.json,
     tools/gpu_world_pmc.sh + tools/world_pmc_json.py) / the launch time
     measured here; traffic = its PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE."""
-    path = os.path.join(REPO, "profiles", "r02", f"world_pmc_{scene}.json")
+    path = evidence(f"world_pmc_{scene}.json")
     bound = ("valu-issue (wave-uniform scalar-loaded records" +
              ("; wave-cooperative BVH traversal)" if info["nodes"] else "; linear list, no BVH)"))
     try:
@@ -192,7 +195,7 @@ def world_roofline(scene, s, kernel_ms, info):
             "traffic": round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"]),
             "valu_busy_frac_pmc": t["valu_busy_frac"], "wait_frac_of_wave_cycles": t["wait_frac_of_wave_cycles"],
             "valu_per_wave_iteration": t["valu_per_wave_iteration"], "kernel": "world_kernel",
-            "source": f"profiles/r02/world_pmc_{scene}.json"}
+            "source": os.path.relpath(path, REPO)}
 
 
 def world_variant(R, torch, scene, steps, warmup):

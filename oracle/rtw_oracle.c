@@ -12,6 +12,7 @@
 #include "rtw_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -641,6 +642,7 @@ uint64_t ro_tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample) {
   return tierb_state(seed, pixel, sample);
 }
 
+int ro_tb_trace = 0; /* tierb_core.h: per-segment trace on stderr (diagnostics) */
 #define TB_REAL double
 #define TB_SUFFIX _f64
 #define TB_IS_F32 0
@@ -663,4 +665,14 @@ void ro_render_tier_b(const ro_scene *scene, const ro_camera *cam, const ro_para
     tierb_render_f32(scene, cam, p, rgb, mean_out, stats);
   else
     tierb_render_f64(scene, cam, p, rgb, mean_out, stats);
+}
+
+void ro_tierb_samples(const ro_scene *scene, const ro_camera *cam, const ro_params *p, uint32_t y, uint32_t x,
+                      uint32_t s0, uint32_t n, double *out, int trace) {
+  ro_tb_trace = trace;
+  if (p->precision == 1)
+    tierb_samples_f32(scene, cam, p, y, x, s0, n, out);
+  else
+    tierb_samples_f64(scene, cam, p, y, x, s0, n, out);
+  ro_tb_trace = 0;
 }

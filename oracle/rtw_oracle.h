@@ -39,6 +39,11 @@ extern "C" {
 /* Material kinds (material.zig:16-21, texture.zig:10-14 flattened). */
 enum { RO_LAMBERT_SOLID = 0, RO_LAMBERT_CHECKER = 1, RO_METAL = 2, RO_DIELECTRIC = 3 };
 
+/* Chunk of the GPU contract's per-pixel sum when params.chunk == 0 (rtw_hip.h
+ * RTW_DEFAULT_CHUNK): chunks of 32 samples summed in order; spp <= 32 is the
+ * reference's own sequential sum (main.zig:388-393). */
+#define RO_DEFAULT_CHUNK 32u
+
 typedef struct {
   double c0[3];     /* Sphere.center / MovingSphere.center0 */
   double c1[3];     /* MovingSphere.center1 (== c0 for static spheres) */
@@ -75,7 +80,7 @@ typedef struct {
   uint64_t seed;
   double background[3];
   uint32_t row_begin, row_stride, row_count; /* image rows (top-first) rendered */
-  uint32_t chunk;             /* samples per accumulation chunk (0 = spp) */
+  uint32_t chunk;             /* samples per accumulation chunk (0 = RO_DEFAULT_CHUNK, the GPU's default) */
   uint32_t precision;         /* 0 = f64, 1 = f32-hybrid */
   uint32_t threads;           /* OpenMP threads (0 = default) */
 } ro_params;
@@ -142,6 +147,10 @@ void ro_render_tier_b(const ro_scene *scene, const ro_camera *cam, const ro_para
 
 /* Quantise one channel exactly as main.zig:395-400. */
 uint8_t ro_quantize(double c, double scale);
+/* Diagnostics: Tier-B radiance of samples s0 .. s0+n-1 of pixel (row y
+ * top-first, column x) -> out[n][3]; trace != 0 prints every segment. */
+void ro_tierb_samples(const ro_scene *scene, const ro_camera *cam, const ro_params *p, uint32_t y, uint32_t x,
+                      uint32_t s0, uint32_t n, double *out, int trace);
 
 #ifdef __cplusplus
 }

@@ -105,6 +105,8 @@ def lib():
         L.ro_render_tier_a_ex.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3, C.c_uint32,
                                           C.c_uint32, C.c_uint32, C.c_uint32, U64x4, C.c_void_p, C.c_void_p,
                                           C.POINTER(Stats), C.c_uint32, C.c_uint32]
+        L.ro_tierb_samples.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.c_uint32,
+                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]
         L.ro_quantize.restype = C.c_uint8
         L.ro_quantize.argtypes = [C.c_double, C.c_double]
         _lib = L
@@ -321,6 +323,16 @@ def render_tier_b(scene: Scene, cam: Camera, width: int, height: int, spp: int, 
     if want_mean:
         return out, mean, st.as_dict()
     return out, st.as_dict()
+
+
+def tierb_samples(scene: Scene, cam: Camera, width: int, height: int, y: int, x: int, s0: int, n: int,
+                  depth: int = 50, seed: int = 42, bg=COVER_BG, precision: int = 0, trace: bool = False) -> np.ndarray:
+    """Diagnostics: Tier-B radiance of samples s0 .. s0+n-1 of pixel (row y,
+    top-first; column x) -> (n, 3) f64; trace prints every segment on stderr."""
+    p = Params(width, height, max(1, s0 + n), depth, seed, (C.c_double * 3)(*bg), y, 1, 1, 0, precision, 1)
+    out = np.zeros((n, 3), np.float64)
+    lib().ro_tierb_samples(C.byref(scene), C.byref(cam), C.byref(p), y, x, s0, n, out.ctypes.data, int(trace))
+    return out
 
 
 def write_ppm(path: str, img: np.ndarray):

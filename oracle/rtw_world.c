@@ -508,7 +508,7 @@ static V sample_b(const rw_world *w, const ro_camera *cam, const ro_params *p, V
 void rw_render_tier_b(const rw_world *w, const ro_camera *cam, const ro_params *p, uint8_t *rgb,
                       float *mean_out, ro_stats *stats) {
   const uint32_t W = p->width, H = p->height;
-  const uint32_t chunk = p->chunk ? p->chunk : p->spp;
+  const uint32_t chunk = p->chunk ? p->chunk : RO_DEFAULT_CHUNK; /* the GPU contract's default (rtw_hip.h RTW_DEFAULT_CHUNK) */
   const double scale = 1.0 / (double)p->spp;
   const V bg = vld(p->background);
   ro_stats total;

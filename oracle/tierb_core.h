@@ -245,6 +245,10 @@ static TBF(V) TBF(sample)(const TBF(Scene) *S, const ro_params *p, uint32_t i, u
       if ((int)k == skip) continue;
       if (TBF(test)(&S->sph[k], o, d, time, a, tmin, &tmax)) hit = (int)k;
     }
+    if (ro_tb_trace)
+      fprintf(stderr, "[tierb] s %u depth %u o %.17g %.17g %.17g d %.17g %.17g %.17g t %.17g hit %d tmax %.17g\n",
+              s_idx, depth, (double)o.x, (double)o.y, (double)o.z, (double)d.x, (double)d.y, (double)d.z,
+              (double)time, hit, (double)tmax);
     if (hit < 0) return TBF(mulv)(T, S->bg); /* miss: background */
     /* hit record for the winner (hittable.zig:118-128 / :189-198) */
     const TBF(Sph) *sp = &S->sph[hit];
@@ -299,12 +303,27 @@ static TBF(V) TBF(sample)(const TBF(Scene) *S, const ro_params *p, uint32_t i, u
   return TBF(mk)(0, 0, 0); /* depth exhausted: main.zig:105-108 */
 }
 
+/* Diagnostics (tests / tools only): the radiance of samples s0 .. s0+n-1 of
+ * one pixel (image row y top-first, column x), n x 3 doubles. */
+static void TBF(tierb_samples)(const ro_scene *sc, const ro_camera *cam, const ro_params *p, uint32_t y, uint32_t x,
+                               uint32_t s0, uint32_t n, double *out) {
+  TBF(Scene) *S = (TBF(Scene) *)malloc(sizeof(TBF(Scene)));
+  TBF(prep)(S, sc, cam, p->background);
+  ro_stats st;
+  memset(&st, 0, sizeof(st));
+  for (uint32_t k = 0; k < n; ++k) {
+    const TBF(V) c = TBF(sample)(S, p, x, p->height - 1 - y, (uint64_t)y * p->width + x, s0 + k, &st);
+    out[3 * k] = (double)c.x, out[3 * k + 1] = (double)c.y, out[3 * k + 2] = (double)c.z;
+  }
+  free(S);
+}
+
 static void TBF(tierb_render)(const ro_scene *sc, const ro_camera *cam, const ro_params *p,
                               uint8_t *rgb, float *mean_out, ro_stats *stats) {
   TBF(Scene) *S = (TBF(Scene) *)malloc(sizeof(TBF(Scene)));
   TBF(prep)(S, sc, cam, p->background);
   const uint32_t W = p->width, H = p->height;
-  const uint32_t chunk = p->chunk ? p->chunk : p->spp;
+  const uint32_t chunk = p->chunk ? p->chunk : RO_DEFAULT_CHUNK; /* the GPU contract's default (rtw_hip.h RTW_DEFAULT_CHUNK) */
   const double scale = 1.0 / (double)p->spp;
   ro_stats total;
   memset(&total, 0, sizeof(total));

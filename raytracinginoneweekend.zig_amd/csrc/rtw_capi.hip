@@ -19,6 +19,7 @@
 #include "rtw_hip.h"
 #include "rtw_cull.hpp"
 #include "rtw_internal.hpp"
+#include "rtw_math.hpp"
 
 namespace {
 
@@ -559,6 +560,8 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
   a.tiles_x = (p->width + rtwk::kTileW - 1) / rtwk::kTileW;
   const uint32_t tiles_y = (p->row_count + rtwk::kTileH - 1) / rtwk::kTileH;
   a.total_units = a.tiles_x * tiles_y * 64u * a.n_chunks;
+  const rtwm::UDivMagic mu = rtwm::udiv_magic(rtwk::kTileW * rtwk::kTileH * a.n_chunks), mt = rtwm::udiv_magic(a.tiles_x);
+  a.upt_m = mu.m, a.upt_sh = mu.sh, a.tx_m = mt.m, a.tx_sh = mt.sh;
   a.seed_base = splitmix_first(p->seed);
   a.partial = reinterpret_cast<double*>(ws + L.partial_off);
   a.counter = reinterpret_cast<uint32_t*>(ws + L.counter_off);

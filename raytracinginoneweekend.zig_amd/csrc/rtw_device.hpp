@@ -87,6 +87,9 @@ constexpr int kVarBatchDecode = 1048576;
 // a wave skips a cluster's member pretests when every lane's line provably
 // misses the cluster's bounding sphere.
 constexpr int kVarCluster = 2097152;
+// Measurement only (phase duplication): the clustered path's survivor
+// loop runs twice, the first pass's result discarded (same image).
+constexpr int kVarDupSurvivors = 8388608;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
@@ -131,15 +134,26 @@ __device__ __forceinline__ uint32_t f64_long_lz(uint64_t draw_state) {  // proba
   }
   return lz;
 }
+// High word of Random.float(f64) for the drawn word's high half `hi` and its
+// leading-zero count `lz`: in the common case (leading one in the top 12
+// bits) three VALU ops — ffbh (clz without the zero fix: the rare branch
+// overrides it), and_or for the mantissa and the exponent base, the exponent.
+__device__ __forceinline__ uint32_t f64_hi_bits(uint32_t hi, uint32_t lz) {
+  // ((1022 - lz) << 20) | (hi & 0xFFFFF) as one v_bfi_b32 on the exponent
+  // field (the compiler turns the or into and + sub + add: 4 ops, not 3)
+  const uint32_t e = (1022u - lz) << 20;
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x000FFFFFu), "v"(hi), "v"(e));
+  return r;
+}
 __device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
   const uint64_t v = sm_next(st);
   const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
   // exponent = 1022 - clz(v); mantissa = low 52 bits.  Common case: the
   // leading one is in the top 12 bits, i.e. in `hi`.
-  uint32_t lz = (uint32_t)__clz((int)hi);
+  uint32_t lz = (uint32_t)__builtin_clz(hi);  // (hi == 0: undefined, overridden below)
   if (__builtin_expect(hi < 0x00100000u, 0)) lz = f64_long_lz(st);
-  const uint32_t bhi = ((1022u - lz) << 20) | (hi & 0x000FFFFFu);
-  return __hiloint2double((int)bhi, (int)lo);
+  return __hiloint2double((int)f64_hi_bits(hi, lz), (int)lo);
 }
 __device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
   const uint64_t v = sm_next(st);
@@ -152,6 +166,40 @@ __device__ __forceinline__ float rnd_f32(uint64_t& st) {  // Random.float(f32)
   const uint32_t bits = ((126u - lz) << 23) | ((uint32_t)v & ((1u << 23) - 1));
   return __uint_as_float(bits);
 }
+// Three consecutive draws (states s + gamma, s + 2 gamma, s + 3 gamma) as
+// Random.float(f64) (rnd_f64 x 3, the same bits); the rare long-leading-zero
+// fix-up (probability 3 * 2^-12) takes one branch for the three.  s2: the
+// state after the second draw.
+__device__ __forceinline__ void rnd3_f64(uint64_t s, double& a, double& b, double& c, uint64_t& s2) {
+  const uint64_t t1 = s + kGamma, t2 = t1 + kGamma, t3 = t2 + kGamma;
+  s2 = t2;
+  const uint64_t v1 = sm_mix(t1), v2 = sm_mix(t2), v3 = sm_mix(t3);
+  const uint32_t h1 = (uint32_t)(v1 >> 32), h2 = (uint32_t)(v2 >> 32), h3 = (uint32_t)(v3 >> 32);
+  uint32_t z1 = (uint32_t)__builtin_clz(h1), z2 = (uint32_t)__builtin_clz(h2), z3 = (uint32_t)__builtin_clz(h3);
+  if (__builtin_expect(min(min(h1, h2), h3) < 0x00100000u, 0)) {
+    if (h1 < 0x00100000u) z1 = f64_long_lz(t1);
+    if (h2 < 0x00100000u) z2 = f64_long_lz(t2);
+    if (h3 < 0x00100000u) z3 = f64_long_lz(t3);
+  }
+  a = __hiloint2double((int)f64_hi_bits(h1, z1), (int)(uint32_t)v1);
+  b = __hiloint2double((int)f64_hi_bits(h2, z2), (int)(uint32_t)v2);
+  c = __hiloint2double((int)f64_hi_bits(h3, z3), (int)(uint32_t)v3);
+}
+__device__ __forceinline__ void rnd3_f32(uint64_t s, float& a, float& b, float& c, uint64_t& s2) {
+  uint64_t t = s;
+  a = rnd_f32(t);
+  b = rnd_f32(t);
+  s2 = t;
+  c = rnd_f32(t);
+}
+template <typename R>
+__device__ __forceinline__ void rnd3(uint64_t s, R& a, R& b, R& c, uint64_t& s2) {
+  if constexpr (sizeof(R) == 8)
+    rnd3_f64(s, a, b, c, s2);
+  else
+    rnd3_f32(s, a, b, c, s2);
+}
+
 template <typename R>
 __device__ __forceinline__ R rnd(uint64_t& st);
 template <>
@@ -242,6 +290,18 @@ struct Lane {
   int skip;
 };
 
+// Wave votes on a bool, straight to the lane-mask builtin: HIP's __ballot /
+// __any / __all take an int, and the bool -> int -> bool round trip costs a
+// v_cndmask + v_cmp per vote where the predicate crosses a block.  Over the
+// ACTIVE lanes, as __ballot / __any / __all.
+__device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ bool wall(bool p) { return __builtin_amdgcn_ballot_w64(!p) == 0; }
+// Population count of a lane mask as two 32-bit counts (scalar s_bcnt1_i32_b32;
+// the 64-bit form's i64 result turns compares of counts into VALU ops).
+__device__ __forceinline__ uint32_t popc64(uint64_t m) {
+  return (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32));
+}
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -265,6 +325,18 @@ struct CoopSlots {
 };
 constexpr size_t kCoopBytesPerWave = sizeof(CoopSlots);
 static_assert(kCoopBytesPerWave * (kTraceBlock / 64) == kCoopLdsBytes, "rtw_internal.hpp kCoopLdsBytes");
+
+// Lane (addr >> 2) & 63's value of x (ds_bpermute; __shfl without its
+// width arithmetic).
+__device__ __forceinline__ float bperm(uint32_t addr, float x) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute((int)addr, __float_as_int(x)));
+}
+__device__ __forceinline__ double bperm(uint32_t addr, double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)(uint32_t)b);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)(uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 template <typename R, int D>
 __device__ __forceinline__ bool in_unit_ball(const R (&x)[D]) {
@@ -302,7 +374,7 @@ __device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], 
   uint32_t nextq = 0;  // candidates are counted from B = st
   while (P) {
     const uint32_t m = (uint32_t)__popcll(P);
-    const uint32_t lc = 31u - (uint32_t)__clz((int)(64u / m));  // c = 2^lc, c*m <= 64
+    const uint32_t lc = (uint32_t)__clz((int)(m - 1u)) - 26u;  // c = 2^lc = 2^floor(log2(64/m)), c*m <= 64
     const uint32_t r = mbcnt64(P);
     if (pending) {
       slots->st[r] = st;
@@ -323,12 +395,12 @@ __device__ __forceinline__ void coop_reject(bool need, uint64_t& st, R (&x)[D], 
     const uint64_t acc = __ballot(ok);
     wave_lds_sync();  // slots are rewritten next round
     const uint32_t first = (r << lc) & 63u;  // pending lanes: r*c < 64
-    const uint64_t mine = lc == 6u ? acc : (acc >> first) & ((1ull << (1u << lc)) - 1ull);
-    const uint32_t jj = mine ? (uint32_t)__builtin_ctzll(mine) : 0u;
-    const int src = (int)(first + jj);
+    const uint64_t mine = (acc >> first) & (~0ull >> (64u - (1u << lc)));
+    const uint32_t jj = (uint32_t)__builtin_ctzll(mine);  // (mine == 0: unused)
+    const uint32_t addr = ((first + jj) & 63u) << 2;
     R z[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) z[i] = __shfl(y[i], src);
+    for (int i = 0; i < D; ++i) z[i] = bperm(addr, y[i]);
     if (pending) {
       if (mine) {
 #pragma unroll
@@ -366,56 +438,62 @@ __device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R 
                                                   CoopSlots* slots, uint32_t lid) {
   bool pending = false;
   if (dim != 0u) {  // round 0: every requesting lane its own first candidate
-    uint64_t s = st;
-    const R r0 = rnd<R>(s), r1 = rnd<R>(s);
-    const uint64_t s2 = s;
-    const R r2 = rnd<R>(s);
+    R r0, r1, r2;
+    uint64_t s2;
+    rnd3<R>(st, r0, r1, r2, s2);
     x[0] = fma(r0, (R)2, (R)-1);  // randomReal(-1, 1) (rrange_m11)
     x[1] = fma(r1, (R)2, (R)-1);
     x[2] = fma(r2, (R)2, (R)-1);
     raw = dim == 1u ? r0 : r2;
-    st = dim == 3u ? s : (dim == 2u ? s2 : st);
+    st = dim == 3u ? s2 + kGamma : (dim == 2u ? s2 : st);
     pending = dim >= 2u && !in_ball_dim<R>(dim, x[0], x[1], x[2]);
   }
   uint64_t P = __ballot(pending);
   uint32_t nextq = 0;  // candidates are counted from B = st
   while (P) {
-    const uint32_t m = (uint32_t)__popcll(P);
-    const uint32_t lc = 31u - (uint32_t)__clz((int)(64u / m));  // c = 2^lc, c*m <= 64
+    const uint32_t m = (uint32_t)__popcll(P);  // wave-uniform (scalar)
+    // c = 2^lc = 2^floor(log2(64/m)) = 2^(6 - ceil(log2 m)) (c*m <= 64): one
+    // scalar clz instead of a division (clz(0) = 32: m = 1 gives lc = 6)
+    const uint32_t lc = (uint32_t)__clz((int)(m - 1u)) - 26u;
     const uint32_t r = mbcnt64(P);
     if (pending) {
       slots->st[r] = st;
       slots->q[r] = nextq | (dim << 24);
     }
     wave_lds_sync();
+    // Every lane evaluates a candidate (lanes past the dealt ones repeat the
+    // last pending lane's slot and never accept): no divergent branch, no
+    // zero-initialised copies.
     const uint32_t orank = lid >> lc;
-    bool ok = false;
-    R y[3] = {(R)0, (R)0, (R)0}, yraw = (R)0;
-    if (orank < m) {
-      const uint32_t qw = slots->q[orank];
-      const uint32_t d = qw >> 24;
-      uint64_t s = slots->st[orank] + (uint64_t)(d * ((qw & 0xFFFFFFu) + (lid & ((1u << lc) - 1u)))) * kGamma;
-      y[0] = rrange_m11<R>(s);
-      y[1] = rrange_m11<R>(s);
-      yraw = rnd<R>(s);
-      y[2] = fma(yraw, (R)2, (R)-1);
-      ok = in_ball_dim<R>(d, y[0], y[1], y[2]);
-    }
+    const uint32_t ork = min(orank, m - 1u);
+    const uint32_t qw = slots->q[ork];
+    const uint32_t d = qw >> 24;
+    const uint64_t sb = slots->st[ork] + (uint64_t)(d * ((qw & 0xFFFFFFu) + (lid & ((1u << lc) - 1u)))) * kGamma;
+    R y0, y1, yraw;
+    uint64_t s2;
+    rnd3<R>(sb, y0, y1, yraw, s2);
+    y0 = fma(y0, (R)2, (R)-1);
+    y1 = fma(y1, (R)2, (R)-1);
+    const R y2f = fma(yraw, (R)2, (R)-1);
+    const bool ok = (orank < m) & in_ball_dim<R>(d, y0, y1, y2f);
+    // dim 3 takes the third coordinate, dim 2 the spare third draw as its
+    // time draw (x[2] is unspecified for dim 2, raw unused for dim 3)
+    const R y2 = d == 3u ? y2f : yraw;
     const uint64_t acc = __ballot(ok);
     wave_lds_sync();  // slots are rewritten next round
-    const uint32_t first = (r << lc) & 63u;  // pending lanes: r*c < 64
-    const uint64_t mine = lc == 6u ? acc : (acc >> first) & ((1ull << (1u << lc)) - 1ull);
-    const uint32_t jj = mine ? (uint32_t)__builtin_ctzll(mine) : 0u;
-    const int src = (int)(first + jj);
-    R z[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) z[i] = __shfl(y[i], src);
-    const R zraw = __shfl(yraw, src);
+    // the owner's c candidates are lanes [first, first + c): its lowest
+    // accepted one (pending lanes: r*c < 64; the mask is wave-uniform)
+    const uint32_t first = (r << lc) & 63u;
+    const uint64_t mine = (acc >> first) & (~0ull >> (64u - (1u << lc)));
+    const uint32_t jj = (uint32_t)__builtin_ctzll(mine);  // (mine == 0: unused)
+    const uint32_t addr = ((first + jj) & 63u) << 2;     // ds_bpermute byte address of the source lane
+    const R z0 = bperm(addr, y0), z1 = bperm(addr, y1), z2 = bperm(addr, y2);
     if (pending) {
       if (mine) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) x[i] = z[i];
-        raw = zraw;
+        x[0] = z0;
+        x[1] = z1;
+        x[2] = z2;
+        raw = z2;
         st += (uint64_t)(dim * (nextq + jj + 1u)) * kGamma;
         pending = false;
       } else {
@@ -905,6 +983,15 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
           }
           if constexpr (STATS) st.cull_lanes += __popc(m0) + __popc(m1);
           RTW_STAMP(2)
+          if constexpr ((VAR & kVarDupSurvivors) != 0) {  // measurement: the survivors' exact tests twice
+            int h2 = hit, o2 = hit_orig;
+            R t2 = tmax;
+            bool n2 = nan_seen;
+            uint32_t q0 = m0, q1 = m1;
+            asm volatile("" : "+v"(q0), "+v"(q1));
+            run_survivors(q0, q1, cb * CS, true);
+            hit = h2, hit_orig = o2, tmax = t2, nan_seen = n2;
+          }
           run_survivors(m0, m1, cb * CS, true);
           RTW_STAMP(6)
         }
@@ -977,6 +1064,11 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
   const V3<R> rs = mk(b3[0], b3[1], b3[2]);
   const V3<R> nv = normalized_rn<R, VAR>(kind <= 1u ? rs : L.d);
   const V3<R> ud = nv;
+  // Metal and Dielectric share reflect(ud, normal) (material.zig:112-114) and
+  // its dot product (the wave runs both branches): the Dielectric's
+  // dot(-ud, normal) (:75) is exactly -dun (negation commutes with rounding).
+  const R dun = dot(ud, normal);
+  const V3<R> refl = sub(ud, mul(normal, (R)2 * dun));
   V3<R> ndir, att;
   bool absorbed = false;
   if (kind <= 1u) {  // Lambertian (material.zig:44-52)
@@ -987,14 +1079,13 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
     if (kind == 1u && rtwm::checker_odd((double)((R)10 * p.x), (double)((R)10 * p.y), (double)((R)10 * p.z)))
       att = ld3(mp + 3);
   } else if (kind == 2u) {  // Metal (material.zig:59-65)
-    const V3<R> refl = sub(ud, mul(normal, (R)2 * dot(ud, normal)));
     ndir = add(refl, mul(rs, mp[6]));
     att = ld3(mp);
     absorbed = !(dot(refl, normal) > (R)0);
   } else {  // Dielectric (material.zig:72-91); mp[6] = RN(1/ir)
     const R ir = mp[7];
     const R ratio = front ? mp[6] : ir;
-    const R cos_t = fmin(dot(mul(ud, (R)-1), normal), (R)1);
+    const R cos_t = fmin(-dun, (R)1);
     const R sin_t = sqrt_k<R, VAR>((R)1 - cos_t * cos_t);
     bool refr = false;
     if (ratio * sin_t <= (R)1) {
@@ -1015,13 +1106,12 @@ __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, i
         refr = refl_p < rnd<R>(L.rs);
       }
     }
-    if (refr) {  // refract (material.zig:116-121)
-      const R ct = fmin(dot(mul(ud, (R)-1), normal), (R)1);
-      const V3<R> perp = mul(add(ud, mul(normal, ct)), ratio);
+    if (refr) {  // refract (material.zig:116-121); its cos_theta is cos_t
+      const V3<R> perp = mul(add(ud, mul(normal, cos_t)), ratio);
       const V3<R> par = mul(normal, -sqrt_k<R, VAR>(fabs((R)1 - norm2(perp))));
       ndir = add(perp, par);
     } else {
-      ndir = sub(ud, mul(normal, (R)2 * dot(ud, normal)));
+      ndir = refl;
     }
     att = mk((R)1, (R)1, (R)1);
   }

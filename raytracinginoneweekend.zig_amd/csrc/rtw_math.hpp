@@ -123,4 +123,27 @@ RTW_HD double sqrt_rn(double x) {
 #endif
 }
 
+// 4. udiv(n, m, sh): n / d for every 32-bit n, given the (m, sh) of
+//    udiv_magic(d) (Granlund-Montgomery round-up method, Hacker's Delight
+//    10-8): l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1,
+//    q = (t + ((n - t) >> 1)) >> (l - 1) with t = mulhi(m, n); d = 1 is
+//    encoded sh = 32 (q = n).  Five integer ops instead of the ~15 of the
+//    compiler's division by a runtime divisor (the divisors are per-render
+//    constants: the work-unit decode).  tests/test_math_host.py checks it.
+struct UDivMagic {
+  uint32_t m, sh;
+};
+inline UDivMagic udiv_magic(uint32_t d) {  // host side, d >= 1
+  if (d == 1) return {0u, 32u};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = (((1ull << l) - d) << 32) / d + 1;
+  return {(uint32_t)m, l - 1};
+}
+RTW_HD uint32_t udiv(uint32_t n, uint32_t m, uint32_t sh) {
+  const uint32_t t = (uint32_t)(((uint64_t)m * n) >> 32);
+  const uint32_t q = (t + ((n - t) >> 1)) >> (sh & 31u);
+  return sh == 32u ? n : q;
+}
+
 }  // namespace rtwm

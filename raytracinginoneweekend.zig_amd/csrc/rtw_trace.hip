@@ -122,10 +122,10 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
             c = in_cur ? cur_c : nb_c;
           } else {
             const uint32_t units_per_tile = kTileW * kTileH * RTW_KA(n_chunks);
-            const uint32_t tile = unit / units_per_tile;
+            const uint32_t tile = rtwm::udiv(unit, RTW_KA(upt_m), RTW_KA(upt_sh));  // unit / units_per_tile
             const uint32_t r = unit - tile * units_per_tile;
             c = r >> 6;
-            ty = tile / RTW_KA(tiles_x);
+            ty = rtwm::udiv(tile, RTW_KA(tx_m), RTW_KA(tx_sh));  // tile / tiles_x
             tx = tile - ty * RTW_KA(tiles_x);
           }
           const uint32_t px = tx * kTileW + (l & 7u);

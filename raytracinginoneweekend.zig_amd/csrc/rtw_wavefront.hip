@@ -63,11 +63,11 @@ template <typename R>
 __device__ __forceinline__ bool decode_unit(const TraceArgs<R>& A, uint32_t unit, uint32_t& px, uint32_t& ly,
                                             uint32_t& c) {
   const uint32_t upt = kTileW * kTileH * A.n_chunks;
-  const uint32_t tile = unit / upt;
+  const uint32_t tile = rtwm::udiv(unit, A.upt_m, A.upt_sh);  // unit / upt
   const uint32_t r = unit - tile * upt;
   c = r >> 6;
   const uint32_t l = r & 63u;
-  const uint32_t ty = tile / A.tiles_x;
+  const uint32_t ty = rtwm::udiv(tile, A.tx_m, A.tx_sh);  // tile / tiles_x
   const uint32_t tx = tile - ty * A.tiles_x;
   px = tx * kTileW + (l & 7u);
   ly = ty * kTileH + (l >> 3);
@@ -249,7 +249,12 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
     A.home_unit[slot] = unit;
     A.home_s[slot] = s;
     double* hs = A.home_sum + 3 * (size_t)slot;
-    hs[0] = hs[1] = hs[2] = 0.0;
+    // A zero the optimiser cannot hoist: hoisted out of the kernel's loop, the
+    // constant vector of this store was kept in scratch (24 B per lane written
+    // every launch: ~20 GB per frame of the fused engine's PMC traffic).
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    hs[0] = hs[1] = hs[2] = z;
     need_sample = true;
   }
   if (need_sample) start_path(A.t, unit, s, L);

@@ -177,6 +177,21 @@ __device__ __forceinline__ bool prim_root(const WV& W, const PrimRec& q, V o, V 
   return root_obj<false, FEAT>(q, s, time, tmin, t);
 }
 
+// fmaxf / fminf of two quiet operands as one v_max_f32 / v_min_f32: the
+// compiler otherwise re-quiets (v_max x, x) the loop-carried tmin / tmax
+// bounds on every node visit (IEEE mode); the instruction's NaN rule is
+// fmaxf's (a quiet NaN operand yields the other one).
+__device__ __forceinline__ float max_q(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float min_q(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // The adjacent f32 toward +inf / -inf (finite or infinite x; NaN kept).
 __device__ __forceinline__ float next_up(float x) {
   if (!(x < __builtin_inff())) return x;
@@ -284,6 +299,9 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   const rtwc::LaneCull lc = rtwc::lane_cull((float)o.x, (float)o.y, (float)o.z, af, W.cull_cmax);
   const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, W.cull_rho);
   const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(W.cull));
+  // Lane masks, fixed for the traversal (its control is wave-uniform): the
+  // votes below combine them with one compare's ballot in scalar ops.
+  const uint64_t act = wballot(true), cull_ok = wballot(lc.ok);
   uint32_t sp = 0, node = 0;  // wave-uniform
 #if RTW_WORLD_TOPCACHE
   uint32_t top = 0;  // the stack's top entry (valid while sp > 0); stack[0 .. sp-1] hold the ones below it
@@ -294,8 +312,8 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     if ((FEAT & ~kFeatImage) == 0 && (ref & kCullBit)) {  // sphere worlds (the other sets ignore the bit)
       const f2 x = cull_pair<1>(ld_pair(ct, first), bc((float)o.x), bc((float)o.y), bc((float)o.z), bc((float)d.x),
                                 bc((float)d.y), bc((float)d.z), bc(lk.na), bc(lk.k), bc((float)time));
-      need0 = __ballot(!lc.ok || !(x.x < 0.0f)) != 0;
-      need1 = __ballot(!lc.ok || !(x.y < 0.0f)) != 0;
+      need0 = (act & ~(cull_ok & wballot(x.x < 0.0f))) != 0;  // some lane not proven to miss
+      need1 = (act & ~(cull_ok & wballot(x.y < 0.0f))) != 0;
     }
     for (uint32_t k = first; k < first + cnt; ++k) {
       if (!(k == first ? need0 : (k == first + 1 ? need1 : true))) continue;  // wave-uniform
@@ -318,7 +336,10 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   };
   for (;;) {
     if (MODE == 1) ++nv;
-    const RTW_CONST float* nd = cn + kNodeWords * node;
+    // 32-bit byte offset: the node's scalar loads take it as their SGPR offset
+    const RTW_CONST float* nd =
+        reinterpret_cast<const RTW_CONST float*>(reinterpret_cast<const RTW_CONST char*>(cn) + (node << 6));
+    static_assert(kNodeWords * 4 == 64, "node record size");
     const uint32_t r0 = __float_as_uint(nd[12]), r1 = __float_as_uint(nd[13]);
     // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3
     const f2 x0 = pfma(f2{nd[0], nd[1]}, ix, oxl), x1 = pfma(f2{nd[6], nd[7]}, ix, oxh);
@@ -328,8 +349,8 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     bool hit[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), fmaxf(fminf(z0[c], z1[c]), tminf));
-      const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), fminf(fmaxf(z0[c], z1[c]), tmaxf));
+      const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), max_q(fminf(z0[c], z1[c]), tminf));
+      const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), min_q(fmaxf(z0[c], z1[c]), tmaxf));
       tn[c] = n;
       hit[c] = n <= f;
     }
@@ -338,8 +359,11 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     if (any1 && (r1 & kLeafBit)) leaf(r1);
     const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
     if (i0 && i1) {  // nearer child first by vote of the lanes that hit
-      const uint32_t v0 = (uint32_t)__popcll(__ballot(hit[0] && (!hit[1] || tn[0] <= tn[1])));
-      const uint32_t v1 = (uint32_t)__popcll(__ballot(hit[1] && (!hit[0] || tn[1] < tn[0])));
+      // votes: lanes hitting child 0 only or nearer-or-equal, and child 1 only or
+      // strictly nearer (masks combined in scalar ops, 32-bit popcounts)
+      const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
+      const uint64_t le = wballot(tn[0] <= tn[1]), gt = wballot(tn[1] < tn[0]);
+      const uint32_t v0 = popc64(b0 & (~b1 | le)), v1 = popc64(b1 & (~b0 | gt));
       const bool first0 = v0 >= v1;
 #if RTW_WORLD_TOPCACHE
       stack[sp++] = top;  // (entry 0 is a dummy when the stack was empty)
@@ -441,18 +465,20 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // globe and Cornell (profiles/r02/world_karg_ab.txt).
   const RTW_CONST WorldView& W =
       opaque((const RTW_CONST WorldArgs*)__builtin_amdgcn_kernarg_segment_ptr())->w;
-  const D margin = A.margin;
+  // The loop's other argument fields too (as the megakernel's VAR bit 1024):
+  // read where used, through the same laundered pointer.
+#define WKA(f) (opaque((const RTW_CONST WorldArgs*)__builtin_amdgcn_kernarg_segment_ptr())->f)
   const uint32_t* order = W.order;
   const uint32_t lid = lane_id();
-  const uint32_t npix = A.t.row_count * A.t.W;
-  const uint32_t units_per_tile = kTileW * kTileH * A.t.n_chunks;
-  const D tmin = A.t.tmin;
   Lane<D> L;
   L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
   L.sx = L.sy = L.sz = 0.0;
   L.rs = 0;
   L.skip = -1;
-  V rad = mk(0.0, 0.0, 0.0);
+  // rayColor forward (main.zig:103-122): a sample's radiance is nonzero only at
+  // the event that ends it (a miss adds T * background, a light T * emitted),
+  // so that one term joins the chunk sum directly: sx + (0 + x) == sx + x
+  // (x >= +0), the oracle's `rad` (rtw_world.c sample_b) without its registers.
   bool have_unit = false, have_ray = false, done = false;
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0;
@@ -467,25 +493,27 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       uint32_t base2 = 0;
       if (n > rem) {
         uint32_t b = 0;
-        if (lid == 0) b = atomicAdd(A.t.counter, kBatch);
+        if (lid == 0) b = atomicAdd(WKA(t.counter), kBatch);
         base2 = __shfl(b, 0);
       }
       if (need) {
         const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
-        if (unit >= A.t.total_units) {
+        if (unit >= WKA(t.total_units)) {
           done = true;
         } else {
-          const uint32_t tile = unit / units_per_tile;
+          const uint32_t units_per_tile = kTileW * kTileH * WKA(t.n_chunks);
+          const uint32_t tile = rtwm::udiv(unit, WKA(t.upt_m), WKA(t.upt_sh));  // unit / units_per_tile
           const uint32_t r = unit - tile * units_per_tile;
-          const uint32_t ty = tile / A.t.tiles_x, tx = tile - ty * A.t.tiles_x;
+          const uint32_t tiles_x = WKA(t.tiles_x);
+          const uint32_t ty = rtwm::udiv(tile, WKA(t.tx_m), WKA(t.tx_sh)), tx = tile - ty * tiles_x;
           const uint32_t px = tx * kTileW + ((r & 63u) & 7u), ly = ty * kTileH + ((r & 63u) >> 3);
-          if (px < A.t.W && ly < A.t.row_count) {
+          if (px < WKA(t.W) && ly < WKA(t.row_count)) {
             have_unit = true;
             L.px = px;
             L.ly = ly;
             L.c = r >> 6;
-            L.s = L.c * A.t.chunk;
-            L.s_end = min(L.s + A.t.chunk, A.t.spp);
+            L.s = L.c * WKA(t.chunk);
+            L.s_end = min(L.s + WKA(t.chunk), WKA(t.spp));
             L.sx = L.sy = L.sz = 0.0;
           }
         }
@@ -511,21 +539,23 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         if (in_unit_ball<D, 2>(dk)) break;
       }
       start_sample_ray<D>(kargs<D>(), L, u, v, dk[0], dk[1]);
-      rad = mk(0.0, 0.0, 0.0);
       have_ray = true;
     }
     // ---- one segment ----
     bool ended = false;
     if (have_ray) {
-      if (L.depth == A.t.max_depth) {
+      if (L.depth == WKA(t.max_depth)) {
         ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
       } else {
         if (MODE == 1) ++n_segments;
         WHit h;
-        closest<MODE, FEAT>(W, margin, stack, L.o, L.d, L.time, tmin, h, n_visits, n_tests);
-        if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, tmin, h);
+        closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests);
+        if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
-          rad = add(rad, mulv(L.T, ld3(opaque(kargs<D>())->bg)));
+          const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
+          L.sx += c.x;
+          L.sy += c.y;
+          L.sz += c.z;
           ended = true;
         } else {
           // Hit record of the winner (object space, then the wrappers back).
@@ -571,56 +601,63 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           }
           if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
           if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
-            rad = add(rad, mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p)));
+            const V c = mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p));
+            L.sx += c.x;
+            L.sy += c.y;
+            L.sz += c.z;
             ended = true;
           } else {
             V ndir, att;
             bool absorbed = false;
-            if (mkind == 0u) {  // Lambertian (material.zig:44-52)
-              D b3[3];
-              for (;;) {  // randomPointInUnitSphere, rand.zig:22-28
-                b3[0] = rrange_m11<D>(L.rs);
-                b3[1] = rrange_m11<D>(L.rs);
-                b3[2] = rrange_m11<D>(L.rs);
-                if (in_unit_ball<D, 3>(b3)) break;
-              }
-              ndir = add(nrm, normalized(mk(b3[0], b3[1], b3[2])));
-              if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
-              att = tex_value<FEAT>(W, mtex, tu, tv, p);
-            } else if (mkind == 1u) {  // Metal (material.zig:59-65)
-              const V ud = normalized(L.d);
-              const V refl = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
-              D b3[3];
+            // Lambertian and Metal draw their unit-ball point in ONE per-lane
+            // rejection loop (randomPointInUnitSphere, rand.zig:22-28; the wave
+            // would otherwise run the two loops one after the other), and every
+            // lane makes one normalisation: the ball point (Lambertian) or the
+            // ray direction (Metal, Dielectric).  Same draws, same operations.
+            D b3[3] = {0.0, 0.0, 0.0};
+            if (mkind <= 1u) {
               for (;;) {
                 b3[0] = rrange_m11<D>(L.rs);
                 b3[1] = rrange_m11<D>(L.rs);
                 b3[2] = rrange_m11<D>(L.rs);
                 if (in_unit_ball<D, 3>(b3)) break;
               }
-              ndir = add(refl, mul(mk(b3[0], b3[1], b3[2]), mp[4]));
-              att = ld3(mp + 1);
-              absorbed = !(dot(refl, nrm) > 0.0);
-            } else {  // Dielectric (material.zig:72-91)
-              const D ir = mp[5];
-              const D ratio = front ? 1.0 / ir : ir;
-              const V ud = normalized(L.d);
-              const D cos_t = fmin(dot(mul(ud, -1.0), nrm), 1.0);
-              const D sin_t = sqrt(1.0 - cos_t * cos_t);
-              bool refr = false;
-              if (ratio * sin_t <= 1.0) {
-                const D r0 = (1.0 - ratio) / (1.0 + ratio);
-                const D r1 = r0 * r0;
-                const D x = 1.0 - cos_t, x2 = x * x;
-                refr = r1 + (1.0 - r1) * (x * (x2 * x2)) < rnd<D>(L.rs);  // Zig pow(x, 5.0)
+            }
+            const V nv = normalized(mkind == 0u ? mk(b3[0], b3[1], b3[2]) : L.d);
+            if (mkind == 0u) {  // Lambertian (material.zig:44-52)
+              ndir = add(nrm, nv);
+              if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
+              att = tex_value<FEAT>(W, mtex, tu, tv, p);
+            } else {
+              // reflect(ud, nrm) (material.zig:112-114) for Metal and Dielectric;
+              // the Dielectric's dot(-ud, nrm) (:75) is exactly -dun
+              const V& ud = nv;
+              const D dun = dot(ud, nrm);
+              const V refl = sub(ud, mul(nrm, 2 * dun));
+              if (mkind == 1u) {  // Metal (material.zig:59-65)
+                ndir = add(refl, mul(mk(b3[0], b3[1], b3[2]), mp[4]));
+                att = ld3(mp + 1);
+                absorbed = !(dot(refl, nrm) > 0.0);
+              } else {  // Dielectric (material.zig:72-91)
+                const D ir = mp[5];
+                const D ratio = front ? 1.0 / ir : ir;
+                const D cos_t = fmin(-dun, 1.0);
+                const D sin_t = sqrt(1.0 - cos_t * cos_t);
+                bool refr = false;
+                if (ratio * sin_t <= 1.0) {
+                  const D r0 = (1.0 - ratio) / (1.0 + ratio);
+                  const D r1 = r0 * r0;
+                  const D x = 1.0 - cos_t, x2 = x * x;
+                  refr = r1 + (1.0 - r1) * (x * (x2 * x2)) < rnd<D>(L.rs);  // Zig pow(x, 5.0)
+                }
+                if (refr) {  // refract (:116-121); its cos_theta is cos_t
+                  const V perp = mul(add(ud, mul(nrm, cos_t)), ratio);
+                  ndir = add(perp, mul(nrm, -sqrt(fabs(1.0 - norm2(perp)))));
+                } else {
+                  ndir = refl;
+                }
+                att = mk(1.0, 1.0, 1.0);
               }
-              if (refr) {
-                const D ct = fmin(dot(mul(ud, -1.0), nrm), 1.0);
-                const V perp = mul(add(ud, mul(nrm, ct)), ratio);
-                ndir = add(perp, mul(nrm, -sqrt(fabs(1.0 - norm2(perp)))));
-              } else {
-                ndir = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
-              }
-              att = mk(1.0, 1.0, 1.0);
             }
             if (absorbed) {
               ended = true;
@@ -634,15 +671,13 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         }
       }
     }
-    if (ended) {  // the sample's radiance joins its chunk sum (main.zig:393)
-      L.sx += rad.x;
-      L.sy += rad.y;
-      L.sz += rad.z;
+    if (ended) {  // (its radiance joined the chunk sum above, main.zig:393)
       L.s++;
       have_ray = false;
       if (MODE == 1) ++n_samples;
       if (L.s == L.s_end) {
-        double* dst = A.t.partial + ((size_t)L.c * npix + (size_t)L.ly * A.t.W + L.px) * 3;
+        const uint32_t npix = WKA(t.row_count) * WKA(t.W);
+        double* dst = WKA(t.partial) + ((size_t)L.c * npix + (size_t)L.ly * WKA(t.W) + L.px) * 3;
         dst[0] = L.sx;
         dst[1] = L.sy;
         dst[2] = L.sz;

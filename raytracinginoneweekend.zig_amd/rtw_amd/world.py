@@ -172,13 +172,14 @@ EARTH_PNG = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path
                          "assets", "sekaichizu.png")
 
 
-def earth_map(path: str = EARTH_PNG) -> np.ndarray:
+def earth_map(path: str | None = None) -> np.ndarray:
     """The reference's globe texture (assets/sekaichizu.png, 500 x 282 RGBA8,
     ocean = alpha 0; loaded by ImageTexture.init, texture.zig:107-119, for
     main.zig:226 and BASELINE configs[4]).  The repo carries the reference's
-    asset file unchanged, with its licence note (assets/LICENSE), so the GPU
-    box renders the real texture; decoded by the library's PNG reader."""
-    return load_png(path)
+    asset file unchanged, with the reference's own note (assets/LICENSE), so
+    the GPU box renders the real texture; RTW_EARTH_MAP names another PNG.
+    Decoded by the library's PNG reader."""
+    return load_png(path or os.environ.get("RTW_EARTH_MAP") or EARTH_PNG)
 
 
 def synthetic_world_map(width: int = 500, height: int = 282) -> np.ndarray:
