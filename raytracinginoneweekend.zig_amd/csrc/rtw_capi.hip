@@ -816,7 +816,9 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
                           (var & rtwk::kVarClusterBit) != 0)
                              ? clusters_usable(sc, cam)
                              : 0u;
-  const size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
+  size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
+  if (p->engine == RTW_ENGINE_MEGAKERNEL && (var & rtwk::kVarHomeLdsBit) != 0)
+    lds += 8 + rtwk::kHomeLdsBytesPerWave * (rtwk::kTraceBlock / 64);  // (8: alignment of the home block)
   if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);
   const int cus = device_cus(dev);

@@ -90,6 +90,9 @@ constexpr int kVarCluster = 2097152;
 // Measurement only (phase duplication): the clustered path's survivor
 // loop runs twice, the first pass's result discarded (same image).
 constexpr int kVarDupSurvivors = 8388608;
+// Megakernel: the lane's unit fields (pixel, chunk, sample end) and f64
+// chunk sum live in LDS instead of VGPRs (rtw_trace.hip HomeLds).
+constexpr int kVarHomeLds = kVarHomeLdsBit;
 template <typename R, int VAR>
 __device__ __forceinline__ R sqrt_k(R x) {
   if constexpr ((VAR & kVarFastSqrt) != 0 && sizeof(R) == 8)
@@ -882,6 +885,9 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
     // Per lane: the exact test on the survivors of a 64-slot block (bit 31-r
     // of m0 / m1 = slot base+r / base+32+r); `clustered`: slots of the
     // clustered tables (T.cpos), else the narrow order of the cull table.
+    // (Dealing the survivors across the wave instead — owners list their
+    // pairs in LDS, every lane tests one with its owner's ray via ds_bpermute
+    // — was 18 % slower: profiles/r03/survivor_compaction_ab.txt.)
     auto run_survivors = [&](uint32_t m0, uint32_t m1, uint32_t base, bool clustered) {
         while (m0 | m1) {  // per lane: the exact test on the survivors
           if constexpr (STATS) {

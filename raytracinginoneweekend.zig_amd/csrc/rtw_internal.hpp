@@ -114,14 +114,18 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 // the kernel argument) + kVarR0Table + kVarMergedStart + kVarPreDraw; f64 also
 // 4 waves/SIMD (4) + kVarFastSqrt + kVarCluster (round 2, +5.4 %,
 // profiles/r02/cluster_ab.txt) + 1024 (the loop's argument fields re-read from
-// the kernel argument too: +0.6 %, profiles/r02/var1024_ab.txt), f32 5
-// waves/SIMD (8).  Every other variant
-// exists only in the -DRTW_MEASURE build.
+// the kernel argument too: +0.6 %, profiles/r02/var1024_ab.txt) + kVarHomeLds
+// (round 3, +0.6 %, profiles/r03/home_lds_ab.txt), f32 5 waves/SIMD (8).
+// Every other variant exists only in the -DRTW_MEASURE build.
 #ifndef RTW_DEFAULT_VAR_F64  // (A/B builds override it)
-#define RTW_DEFAULT_VAR_F64 (4 + 512 + 1024 + 32768 + 131072 + 262144 + 524288 + 2097152)  // 3048964
+#define RTW_DEFAULT_VAR_F64 (4 + 512 + 1024 + 32768 + 131072 + 262144 + 524288 + 2097152 + 16777216)  // 19826180
 #endif
 constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
 constexpr int kVarClusterBit = 2097152;  // rtw_device.hpp kVarCluster (clustered pretest, f64)
+// rtw_device.hpp kVarHomeLds: the lane's unit fields and f64 chunk sum in LDS
+// (megakernel), kHomeLdsBytesPerWave per wave after the scene tables.
+constexpr int kVarHomeLdsBit = 16777216;
+constexpr size_t kHomeLdsBytesPerWave = 2560;
 constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
 bool trace_variant_built(int precision, int var);
 constexpr int kTraceBlock = 256;

@@ -58,6 +58,19 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   CoopSlots* slots = T.slots;
 
   const uint32_t lid = lane_id();
+  // VAR kVarHomeLds: the lane's unit fields (pixel, chunk, sample end) and its
+  // f64 chunk sum live in this wave's LDS home block (SoA, one entry per
+  // lane) instead of 10 VGPRs held across the closest hit; they are touched
+  // only when a unit starts or ends, a sample starts, or a path misses.
+  constexpr bool HOME = (VAR & kVarHomeLds) != 0;
+  double* h_sum = nullptr;    // [3][64]
+  uint32_t* h_u32 = nullptr;  // px[64], ly[64], c[64], s_end[64]
+  if constexpr (HOME) {
+    const size_t off = (size_t)(reinterpret_cast<unsigned char*>(T.cpos + kClusterSlots * S.n_clusters) - lds_raw);
+    unsigned char* hb = lds_raw + ((off + 7) & ~(size_t)7) + (threadIdx.x >> 6) * kHomeLdsBytesPerWave;
+    h_sum = reinterpret_cast<double*>(hb);
+    h_u32 = reinterpret_cast<uint32_t*>(hb + 3 * 64 * 8);
+  }
   // VAR bit 10: the loop's kernel-argument fields are re-read where used
   // (scalar loads through a laundered kernarg pointer) instead of living in
   // SGPRs for the whole kernel: the SGPR budget is the limit (spills become
@@ -132,12 +145,22 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           const uint32_t ly = ty * kTileH + (l >> 3);
           if (px < RTW_KA(W) && ly < RTW_KA(row_count)) {  // else: padding unit, take another
             have_unit = true;
-            L.px = px;
-            L.ly = ly;
-            L.c = c;
             L.s = c * RTW_KA(chunk);
-            L.s_end = min(L.s + RTW_KA(chunk), RTW_KA(spp));
-            L.sx = L.sy = L.sz = 0.0;
+            if constexpr (HOME) {
+              double z = 0.0;  // (laundered: a hoisted constant would hold registers)
+              asm volatile("" : "+v"(z));
+              h_u32[lid] = px;
+              h_u32[64 + lid] = ly;
+              h_u32[128 + lid] = c;
+              h_u32[192 + lid] = min(L.s + RTW_KA(chunk), RTW_KA(spp));
+              h_sum[lid] = h_sum[64 + lid] = h_sum[128 + lid] = z;
+            } else {
+              L.px = px;
+              L.ly = ly;
+              L.c = c;
+              L.s_end = min(L.s + RTW_KA(chunk), RTW_KA(spp));
+              L.sx = L.sy = L.sz = 0.0;
+            }
           }
         }
       }
@@ -157,7 +180,17 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     L.s++;
     have_ray = false;
     if (STATS) st.samples++;
-    if (L.s == L.s_end) {
+    if constexpr (HOME) {
+      if (L.s == h_u32[192 + lid]) {
+        const uint32_t npix = RTW_KA(row_count) * RTW_KA(W);
+        double* dst = RTW_KA(partial) +
+                      ((size_t)h_u32[128 + lid] * npix + (size_t)h_u32[64 + lid] * RTW_KA(W) + h_u32[lid]) * 3;
+        dst[0] = h_sum[lid];
+        dst[1] = h_sum[64 + lid];
+        dst[2] = h_sum[128 + lid];
+        have_unit = false;
+      }
+    } else if (L.s == L.s_end) {
       const uint32_t npix = RTW_KA(row_count) * RTW_KA(W);
       double* dst = RTW_KA(partial) + ((size_t)L.c * npix + (size_t)L.ly * RTW_KA(W) + L.px) * 3;
       dst[0] = L.sx;
@@ -186,9 +219,15 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
     if (hit < 0) {  // miss: background (main.zig:109-112)
       const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
-      L.sx += (double)col.x;
-      L.sy += (double)col.y;
-      L.sz += (double)col.z;
+      if constexpr (HOME) {
+        h_sum[lid] += (double)col.x;
+        h_sum[64 + lid] += (double)col.y;
+        h_sum[128 + lid] += (double)col.z;
+      } else {
+        L.sx += (double)col.x;
+        L.sy += (double)col.y;
+        L.sz += (double)col.z;
+      }
       return 1;
     }
     kind = T.kind[(T.meta[hit] >> 8) & 0xFFFu];
@@ -216,7 +255,13 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       RTW_STAMP(0)
       const bool ns = have_unit && !have_ray;
       R u = (R)0, v = (R)0;
-      if (ns) start_sample_uv<R>(kargs<R>(), L, u, v);
+      if (ns) {
+        if constexpr (HOME) {
+          L.px = h_u32[lid];
+          L.ly = h_u32[64 + lid];
+        }
+        start_sample_uv<R>(kargs<R>(), L, u, v);
+      }
       RTW_STAMP(1)
       // dim: 3 unit ball (Lambertian, Metal), 1 the dielectric's draw, 2 lens disk (+ time)
       constexpr bool PRE = (VAR & kVarPreDraw) != 0;
@@ -394,7 +439,8 @@ static void launch_var(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStre
   X(0) X(1) X(5) X(9) X(16) X(24) X(32) X(36) X(20) X(68) X(72) X(40) X(4) X(8) X(516) X(1540) X(520) X(1544)  \
   X(33284) X(66052) X(131588) X(229892) X(197128) X(164356) X(131592) X(426500) X(393736) X(1999364)         \
   X(1966600) X(950792) X(1016324) X(2064900) X(918020) X(2564) X(4612) X(8708) X(16900)                    \
-  X(950788) X(3047940) /* round-1 f64 default (the r02 A/B baseline), round-2 default before bit 1024 */
+  X(950788) X(3047940) X(3048964) /* round-1 f64 default (the r02 A/B baseline), round-2 default before bit  \
+                                     1024, round-2 default (before kVarHomeLds) */
 #endif
 
 template <bool F32>

@@ -358,9 +358,12 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     if (any0 && (r0 & kLeafBit)) leaf(r0);
     if (any1 && (r1 & kLeafBit)) leaf(r1);
     const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
-    if (i0 && i1) {  // nearer child first by vote of the lanes that hit
-      // votes: lanes hitting child 0 only or nearer-or-equal, and child 1 only or
-      // strictly nearer (masks combined in scalar ops, 32-bit popcounts)
+    if (i0 && i1) {
+      // nearer child first by vote of the lanes that hit: lanes hitting child 0
+      // only or nearer-or-equal, and child 1 only or strictly nearer (masks
+      // combined in scalar ops, 32-bit popcounts).  (Ordering by the wave's
+      // majority ray sign along the split axis instead visits 101 nodes per
+      // segment against 84: 13 % slower, profiles/r03/world_signorder_ab.txt.)
       const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
       const uint64_t le = wballot(tn[0] <= tn[1]), gt = wballot(tn[1] < tn[0]);
       const uint32_t v0 = popc64(b0 & (~b1 | le)), v1 = popc64(b1 & (~b0 | gt));

@@ -1,5 +1,9 @@
 """Wavefront-engine timing of BASELINE configs[1] (1200x675x500, f64): best of
-N renders, HIP events around the bounce loop.  python tools/wf_bench.py [N]"""
+N renders, HIP events around the bounce loop.
+  python tools/wf_bench.py [N] [CFG ...]
+CFG (in-process A/B, configurations interleaved per round): comma-separated
+"paths=<wf_paths>" and environment settings read by the library at each render
+(e.g. "RTW_WF_GRID=4", "RTW_WF_FINISH=0"); "-" is the default configuration."""
 import os
 import sys
 
@@ -11,19 +15,41 @@ import rtw_amd as R  # noqa: E402
 from rtw_amd.device import TorchRenderer  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+cfgs = sys.argv[2:] or ["-"]
 W, spp = 1200, 500
 H = R.image_height(W, 16 / 9)
 sph, mats, _ = R.cover_scene(42)
 cam = R.cover_camera(16 / 9)
 rend = TorchRenderer(sph, mats, 0)
-p = R.make_params(W, H, spp, engine="wavefront")
-rend.render(cam, p)
+base_env = dict(os.environ)
+
+
+def apply(cfg):
+    """Set the configuration's environment; return its params."""
+    os.environ.clear()
+    os.environ.update(base_env)
+    paths = 0
+    for kv in ([] if cfg == "-" else cfg.split(",")):
+        k, v = kv.split("=")
+        if k == "paths":
+            paths = int(v)
+        else:
+            os.environ[k] = v
+    return R.make_params(W, H, spp, engine="wavefront", wf_paths=paths)
+
+
+best = {c: 1e9 for c in cfgs}
+for c in cfgs:  # warm-up (allocations, code objects)
+    rend.render(cam, apply(c))
 torch.cuda.synchronize()
-best = 1e9
 for _ in range(n):
-    t = R.Timer()
-    rend.render(cam, p, timer=t)
-    torch.cuda.synchronize()
-    best = min(best, t.elapsed_ms())
-    t.close()
-print(f"wavefront f64 {best:.3f} ms {W * H * spp / best / 1e3:.0f} Msamples/s", flush=True)
+    for c in cfgs:
+        p = apply(c)
+        t = R.Timer()
+        rend.render(cam, p, timer=t)
+        torch.cuda.synchronize()
+        best[c] = min(best[c], t.elapsed_ms())
+        t.close()
+for c in cfgs:
+    tag = "" if cfgs == ["-"] else f"[{c}] "
+    print(f"wavefront f64 {tag}{best[c]:.3f} ms {W * H * spp / best[c] / 1e3:.0f} Msamples/s", flush=True)
