@@ -428,9 +428,6 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
 // sample's camera ray) in registers; live paths are appended to the output
 // queue WITH their hit, so no separate extend launch re-reads the rays.
 // Per bounce segment: path + hit read (108 B f64), path + hit written.
-#ifndef RTW_WF_STEP_PREFETCH
-#define RTW_WF_STEP_PREFETCH 0
-#endif
 #ifndef RTW_WF_STEP_OCC
 #define RTW_WF_STEP_OCC 5  // profiles/r02/wf_step_ab.txt: 5 waves (32-B spill) ~3 % faster than 4
 #endif
@@ -446,63 +443,11 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R
   const LdsTables<R> T = stage_tables<R>(A.t.sc, lds_raw);
   KStats st;
   static_assert(kSegCap == 64, "one path per lane per segment");
-#if RTW_WF_STEP_PREFETCH
-  // Software-pipelined over the wave's segments: the next segment's paths are
-  // loaded after this segment's shading (whose home-slot loads would otherwise
-  // wait for them: loads complete in order) and arrive during its closest hit.
-  struct Pre {
-    Lane<R> L;
-    uint32_t slot, n_in;
-    int hit;
-    R tmax;
-  };
-  auto fetch = [&](uint32_t seg, Pre& P) {
-    P.n_in = seg < A.n_segs ? A.seg_in[seg] : 0u;
-    P.L = Lane<R>{};
-    P.L.skip = -1;
-    P.slot = 0;
-    P.hit = -1;
-    P.tmax = (R)0;
-    if (lid < P.n_in) {
-      const uint32_t i = seg * kSegCap + lid;
-      load_path(A.in, i, P.L, P.slot);
-      P.hit = A.in.hk[i];
-      P.tmax = A.in.ht[i];
-    }
-  };
-  Pre cur;
-  fetch(wave_id(), cur);
-  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
-    Pre nxt;
-    if (cur.n_in == 0u) {
-      if (lid == 0) A.seg_out[seg] = 0u;
-      fetch(seg + wave_count(), nxt);
-      cur = nxt;
-      continue;
-    }
-    const uint32_t base = seg * kSegCap;
-    uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
-    const bool valid = lid < cur.n_in;
-    Lane<R>& L = cur.L;
-    const bool live = shade_step<R, F32, STATS>(A, T, lid, valid, L, cur.slot, cur.hit, cur.tmax, qnext, qend);
-    fetch(seg + wave_count(), nxt);
-    int nh = -1;
-    R nt = (R)__builtin_huge_val();
-    if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
-    push_path_hit(A.out, base, out_n, live, L, cur.slot, nh, nt);
-    if (lid == 0) {
-      A.seg_out[seg] = out_n;
-      A.seg_resv[2 * seg] = qnext;
-      A.seg_resv[2 * seg + 1] = qend;
-    }
-    cur = nxt;
-  }
-#else
-  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) {
+  auto step_segment = [&](uint32_t seg) {
     const uint32_t n_in = A.seg_in[seg];
     if (n_in == 0u) {
       if (lid == 0) A.seg_out[seg] = 0u;
-      continue;
+      return;
     }
     const uint32_t base = seg * kSegCap;
     uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
@@ -528,8 +473,11 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R
       A.seg_resv[2 * seg] = qnext;
       A.seg_resv[2 * seg + 1] = qend;
     }
-  }
-#endif
+  };
+  // (Segments dealt at run time instead, one ticket of a device counter per
+  // segment, was 2.5x slower: ~16K same-address atomics per launch serialise
+  // at ~8.5 ns each; profiles/r03/wf_dynamic_ab.txt.)
+  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) step_segment(seg);
 }
 
 // ------------------------------------------------------------------ finish --

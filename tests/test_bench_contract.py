@@ -1,16 +1,17 @@
-"""The committed bench line (profiles/r02/bench.json, written by bench.py on an
-MI355X) keeps the driver's contract: the BASELINE metric and unit, whole-job
+"""The committed bench line (profiles/<ROUND>/bench.json, written by bench.py on
+an MI355X) keeps the driver's contract: the BASELINE metric and unit, whole-job
 throughput consistent with ms_per_step, the roofline object (bound, achieved,
 peak, unit, frac = achieved / peak, traffic from the PMC passes) with the
-VALU-issue evidence of profiles/r02/valu_issue.json, the world kernels'
-VALU-issue rooflines (profiles/r02/world_pmc_*.json), and a bounded
-cpu_baseline.  CPU-only: it reads files, it runs nothing."""
+VALU-issue evidence of profiles/<ROUND>/valu_issue.json, the world kernels'
+VALU-issue rooflines (profiles/<ROUND>/world_pmc_*.json), and a bounded
+cpu_baseline; the traffic figures DESIGN.md quotes are the committed PMC
+JSON's.  CPU-only: it reads files, it runs nothing."""
 import json
 import os
 
 from conftest import REPO
 
-ROUND = "r02"
+ROUND = "r03"
 BENCH = os.path.join(REPO, "profiles", ROUND, "bench.json")
 
 
@@ -24,7 +25,7 @@ def source_round(roof, name, key):
     without a traffic_source field: the round whose file holds the value)."""
     if "traffic_source" in roof:
         return roof["traffic_source"].split("/")[1]
-    for rnd in (ROUND, "r01"):
+    for rnd in (ROUND, "r02", "r01"):
         if os.path.exists(os.path.join(REPO, "profiles", rnd, name)) and round(load(name, rnd)[key]) == roof["traffic"]:
             return rnd
     return ROUND
@@ -101,3 +102,20 @@ def test_world_rooflines_are_the_pmc_evidence():
         assert r["traffic"] == round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"])
         # the PMC dispatch and the bench's launch time agree
         assert abs(t["dispatch_ms"] - kms) / kms < 0.1
+
+
+def test_design_traffic_figures_are_the_committed_json():
+    """DESIGN.md §0's PMC traffic table quotes exactly the committed evidence
+    (rounded as printed), so a reader never meets a stale figure."""
+    import re
+    text = open(os.path.join(REPO, "DESIGN.md")).read()
+    keys = {"traffic.json": "traffic_bytes_per_launch", "wf_traffic.json": "traffic_bytes_per_frame"}
+    rows = re.findall(r"^\| [^|`]*\(`profiles/(r\d\d)/(\w+\.json)`\) \| \w+ \| ([\d.]+) (MB|GB) \|", text, re.M)
+    assert len(rows) >= 4, rows
+    for rnd, name, val, unit in rows:
+        assert rnd == ROUND, (rnd, name)
+        t = load(name, rnd)
+        b = t[keys[name]] if name in keys else t["hbm_fetch_bytes"] + t["hbm_write_bytes"]
+        scale = 1e6 if unit == "MB" else 1e9
+        digits = len(val.split(".")[1]) if "." in val else 0
+        assert abs(float(val) - b / scale) <= 0.5 * 10 ** -digits + 1e-12, (name, val, unit, b)

@@ -11,6 +11,8 @@
 #   TESTS="tests/test_gpu_parity.py ..."  pytest -m gpu selection run through
 #                 every build of LIBS before the timing (bit identity)
 #   ROUNDS=3      alternations;  ENVS="lib:RTW_X=1"  extra env per build
+#   PMC="lib_x"   afterwards, the VALU-issue PMC passes of configs[1]
+#                 (tools/gpu_pmc_valu.sh) through each of these builds, TAG=ab_<build>
 # Output: gpurun_out/ab_<ENGINE>.txt (one line per build and round).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -47,5 +49,8 @@ d['f32_hybrid_variant']['value'], d['roofline']['trace_ms_per_launch'])" >> $OUT
           | sed "s/^/$L round $r /" >> $OUT || exit 1 ;;
     esac
   done
+done
+for L in ${PMC:-}; do
+  RTW_LIB_PATH=$P/$L/librtw_hip.so TAG=ab_$L bash tools/gpu_pmc_valu.sh || exit 1
 done
 cat $OUT

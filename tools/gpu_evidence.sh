@@ -17,11 +17,11 @@ TAG=${TAG:-r03}
 for stage in ${STAGES:-tests pmc bench}; do
   case $stage in
     tests)
-      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v -s --durations=15 --timeout 300 --timeout-method thread \
         > gpurun_out/pytest_gpu.log 2>&1 &&
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1 ;;
     pmc)
-      bash tools/gpu_pmc_valu.sh &&
+      TAG=${TAG}v bash tools/gpu_pmc_valu.sh &&
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_fetch -o run \
         --pmc FETCH_SIZE -- python tools/prof_run.py f64 > gpurun_out/pmc_fetch.log 2>&1 &&
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_write -o run \

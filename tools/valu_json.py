@@ -50,6 +50,16 @@ def main():
     res["segments_per_launch"] = SEGMENTS
     res["valu_per_wave_iteration"] = round(res["SQ_INSTS_VALU"] / (SEGMENTS / 64))
     res["valu_busy_frac"] = round(res["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc), 3)
+    # instruction mix per wave-iteration; "other" = moves, selects, compares,
+    # bit operations and lane ops (the VALU classes the SQ does not count apart)
+    wi = SEGMENTS / 64
+    cls = {"f64": ["ADD_F64", "MUL_F64", "FMA_F64", "TRANS_F64"], "f32": ["ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32"],
+           "int": ["INT32", "INT64"], "cvt": ["CVT"]}
+    mix = {k: sum(res.get("SQ_INSTS_VALU_" + c, 0.0) for c in v) / wi for k, v in cls.items()}
+    mix["other"] = res["SQ_INSTS_VALU"] / wi - sum(mix.values())
+    res["valu_mix_per_wave_iteration"] = {k: round(x) for k, x in mix.items()}
+    res["valu_mix_share"] = {k: round(x / (res["SQ_INSTS_VALU"] / wi), 3) for k, x in mix.items()}
+    res["salu_per_wave_iteration"] = round(res["SQ_INSTS_SALU"] / wi)
     res["phase_valu_per_wave_iteration"] = dict(PHASES, variant_measured=516,
                                                 method="phase executed twice on laundered inputs (same image)")
     json.dump(res, open(out, "w"), indent=1)
