@@ -115,7 +115,8 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 // 4 waves/SIMD (4) + kVarFastSqrt + kVarCluster (round 2, +5.4 %,
 // profiles/r02/cluster_ab.txt) + 1024 (the loop's argument fields re-read from
 // the kernel argument too: +0.6 %, profiles/r02/var1024_ab.txt) + kVarHomeLds
-// (round 3, +0.6 %, profiles/r03/home_lds_ab.txt), f32 5 waves/SIMD (8).
+// (round 3, +0.6 %, profiles/r03/home_lds_ab.txt), f32 5 waves/SIMD (8) +
+// kVarHomeLds (+1.3 %, profiles/r03/home_lds_f32_ab.txt).
 // Every other variant exists only in the -DRTW_MEASURE build.
 #ifndef RTW_DEFAULT_VAR_F64  // (A/B builds override it)
 #define RTW_DEFAULT_VAR_F64 (4 + 512 + 1024 + 32768 + 131072 + 262144 + 524288 + 2097152 + 16777216)  // 19826180
@@ -126,7 +127,10 @@ constexpr int kVarClusterBit = 2097152;  // rtw_device.hpp kVarCluster (clustere
 // (megakernel), kHomeLdsBytesPerWave per wave after the scene tables.
 constexpr int kVarHomeLdsBit = 16777216;
 constexpr size_t kHomeLdsBytesPerWave = 2560;
-constexpr int kDefaultVarF32 = 8 + 512 + 131072 + 262144 + 524288;          // 918024
+#ifndef RTW_DEFAULT_VAR_F32  // (A/B builds override it)
+#define RTW_DEFAULT_VAR_F32 (8 + 512 + 131072 + 262144 + 524288 + 16777216)  // 17695240
+#endif
+constexpr int kDefaultVarF32 = RTW_DEFAULT_VAR_F32;
 bool trace_variant_built(int precision, int var);
 constexpr int kTraceBlock = 256;
 // Per-wave LDS slots of coop_reject (rtw_trace.hip CoopSlots: 64 x u64 + 64 x u32).

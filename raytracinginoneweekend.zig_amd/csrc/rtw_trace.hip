@@ -439,8 +439,8 @@ static void launch_var(const TraceArgs<R>& a, uint32_t grid, size_t lds, hipStre
   X(0) X(1) X(5) X(9) X(16) X(24) X(32) X(36) X(20) X(68) X(72) X(40) X(4) X(8) X(516) X(1540) X(520) X(1544)  \
   X(33284) X(66052) X(131588) X(229892) X(197128) X(164356) X(131592) X(426500) X(393736) X(1999364)         \
   X(1966600) X(950792) X(1016324) X(2064900) X(918020) X(2564) X(4612) X(8708) X(16900)                    \
-  X(950788) X(3047940) X(3048964) /* round-1 f64 default (the r02 A/B baseline), round-2 default before bit  \
-                                     1024, round-2 default (before kVarHomeLds) */
+  X(950788) X(3047940) X(3048964) X(918024) /* round-1 f64 default (the r02 A/B baseline), round-2 default  \
+                                     before bit 1024, round-2 f64 / f32 defaults (before kVarHomeLds) */
 #endif
 
 template <bool F32>
