@@ -33,6 +33,18 @@
 
 namespace rtwk {
 
+// MODE 2 (-DRTW_MEASURE, RTW_WORLD_PHASE=1): s_memtime stamps per phase,
+// summed per wave (diagnostic; rtw_world_capi.hip prints the shares).
+#define WSTAMP(slot)                                                             \
+  if constexpr (MODE == 2) {                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    st.ph[slot] += t_ - st.t_last;                                               \
+    st.t_last = t_;                                                              \
+  }
+
 using D = double;
 using V = V3<D>;
 
@@ -237,7 +249,8 @@ __device__ __forceinline__ void seq_hit(const WV& W, const uint32_t* order, V o,
 
 template <int MODE, int FEAT, typename WV>
 __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const V& o, const V& d, D time,
-                                        D tmin, WHit& h, unsigned long long& nv, unsigned long long& nt) {
+                                        D tmin, WHit& h, unsigned long long& nv, unsigned long long& nt,
+                                        KStats& st) {
   h.pos = -1;
   h.orig = -1;
   h.t = (D)__builtin_huge_val();
@@ -307,17 +320,9 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   uint32_t top = 0;  // the stack's top entry (valid while sp > 0); stack[0 .. sp-1] hold the ones below it
 #endif
   auto leaf = [&](uint32_t ref) {
+    WSTAMP(2)  // (MODE 2: node visits up to here)
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & kLeafCountMask;
-    bool need0 = true, need1 = true;
-    if ((FEAT & ~kFeatImage) == 0 && (ref & kCullBit)) {  // sphere worlds (the other sets ignore the bit)
-      const f2 x = cull_pair<1>(ld_pair(ct, first), bc((float)o.x), bc((float)o.y), bc((float)o.z), bc((float)d.x),
-                                bc((float)d.y), bc((float)d.z), bc(lk.na), bc(lk.k), bc((float)time));
-      need0 = (act & ~(cull_ok & wballot(x.x < 0.0f))) != 0;  // some lane not proven to miss
-      need1 = (act & ~(cull_ok & wballot(x.y < 0.0f))) != 0;
-    }
-    for (uint32_t k = first; k < first + cnt; ++k) {
-      if (!(k == first ? need0 : (k == first + 1 ? need1 : true))) continue;  // wave-uniform
-      const PrimRec q = load_rec(pr + kWorldRec * k);
+    auto test_prim = [&](uint32_t k, const PrimRec& q) {
       const int xf = (int)(q.meta0 >> 8) - 1;
       D t;
       if (MODE == 1) ++nt;
@@ -331,12 +336,29 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
         ok = root_obj<false, FEAT>(q, s, time, tmin, t);
       }
       if (ok) accept(h, t, (int)k, (int)q.orig, tmin);
+    };
+    bool need0 = true, need1 = true;
+    if ((FEAT & ~kFeatImage) == 0 && (ref & kCullBit)) {  // sphere worlds (the other sets ignore the bit)
+      const f2 x = cull_pair<1>(ld_pair(ct, first), bc((float)o.x), bc((float)o.y), bc((float)o.z), bc((float)d.x),
+                                bc((float)d.y), bc((float)d.z), bc(lk.na), bc(lk.k), bc((float)time));
+      need0 = (act & ~(cull_ok & wballot(x.x < 0.0f))) != 0;  // some lane not proven to miss
+      need1 = (act & ~(cull_ok & wballot(x.y < 0.0f))) != 0;
+    }
+    // (Loading the first primitive's record together with the pretest record,
+    // one latency instead of two in a row, measured within noise:
+    // profiles/r03/world_leaf_prefetch_ab.txt.)
+    for (uint32_t k = first; k < first + cnt; ++k) {
+      if (!(k == first ? need0 : (k == first + 1 ? need1 : true))) continue;  // wave-uniform
+      test_prim(k, load_rec(pr + kWorldRec * k));
     }
     tmaxf = round_up(h.t);
+    WSTAMP(3)  // leaf primitives
   };
   for (;;) {
     if (MODE == 1) ++nv;
-    // 32-bit byte offset: the node's scalar loads take it as their SGPR offset
+    // 32-bit byte offset: the node's scalar loads take it as their SGPR offset.
+    // (An LDS copy of the top levels, breadth-first, read with broadcast
+    // ds_reads instead: 7 % slower, profiles/r03/world_lds_nodes_ab.txt.)
     const RTW_CONST float* nd =
         reinterpret_cast<const RTW_CONST float*>(reinterpret_cast<const RTW_CONST char*>(cn) + (node << 6));
     static_assert(kNodeWords * 4 == 64, "node record size");
@@ -380,7 +402,10 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     } else if (i1) {
       node = r1;
     } else {
-      if (sp == 0) break;
+      if (sp == 0) {
+        WSTAMP(2)
+        break;
+      }
 #if RTW_WORLD_TOPCACHE
       // The top entry lives in a register: the pop waits on no LDS read; the
       // next top's LDS read is issued now and overlaps this node's loads.
@@ -485,6 +510,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   bool have_unit = false, have_ray = false, done = false;
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0;
+  KStats st;  // MODE 2: phase stamps
+  if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
   for (;;) {
     // ---- take units (wave-uniform; rtw_trace.hip step 1) ----
     const bool need = !have_unit && !done;
@@ -552,7 +579,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       } else {
         if (MODE == 1) ++n_segments;
         WHit h;
-        closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests);
+        WSTAMP(1)  // sample start (+ take units, loop control)
+        closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
         if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
           const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
@@ -674,6 +702,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         }
       }
     }
+    WSTAMP(4)  // hit record, texture, scatter (+ the NaN fallback)
     if (ended) {  // (its radiance joined the chunk sum above, main.zig:393)
       L.s++;
       have_ray = false;
@@ -688,6 +717,11 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       }
     }
   }
+  if constexpr (MODE == 2) {
+    WSTAMP(0)
+    if (lid == 0)
+      for (int i = 0; i < 5; ++i) atomicAdd(A.counts + 8 + i, (unsigned long long)st.ph[i]);
+  }
   if constexpr (MODE == 1) {
     atomicAdd(A.counts + 0, n_samples);
     atomicAdd(A.counts + 1, n_segments);
@@ -700,6 +734,12 @@ size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * (kWorldBlock / 64)
 
 template <int OCC, int FEAT>
 static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
+#ifdef RTW_MEASURE
+  if (mode == 2) {
+    hipLaunchKernelGGL((world_kernel<2, OCC, FEAT>), dim3(grid), dim3(kWorldBlock), lds, s, a);
+    return;
+  }
+#endif
   if (mode == 1)
     hipLaunchKernelGGL((world_kernel<1, OCC, FEAT>), dim3(grid), dim3(kWorldBlock), lds, s, a);
   else

@@ -581,8 +581,10 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   const char* fe = getenv("RTW_WORLD_FEAT");
   const int fs = rtwk::world_feature_set((fe && !std::strcmp(fe, "all")) ? 15u : w->feat);
   static int bpc_cache[16][5] = {};
+  static size_t bpc_lds[16][5] = {};
   const int oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
-  if (bpc_cache[fs][oi] == 0) bpc_cache[fs][oi] = rtwk::world_blocks_per_cu(lds, oi, fs);
+  if (bpc_cache[fs][oi] == 0 || bpc_lds[fs][oi] != lds)
+    bpc_cache[fs][oi] = rtwk::world_blocks_per_cu(lds, oi, fs), bpc_lds[fs][oi] = lds;
   const int bpc = bpc_cache[fs][oi];
   const uint32_t want = (a.t.total_units + 255) / 256;
   const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
@@ -607,6 +609,24 @@ int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params
 int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
                             uint64_t counts_out[4]) {
   if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
+#ifdef RTW_MEASURE
+  // RTW_WORLD_PHASE=1 (diagnostic build): a phase-stamp pass first; its wave-cycle
+  // shares go to stderr (tools/world_bench.py --phase).
+  const char* ph = getenv("RTW_WORLD_PHASE");
+  if (ph && *ph == '1') {
+    int st2 = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 2);
+    if (st2 != RTW_OK) return st2;
+    unsigned long long q[5];
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(q, static_cast<unsigned char*>(ws) + rtw_ws_stats_off(p) + 8 * 8, sizeof(q), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+      return rtw_fail(RTW_EHIP, "world phase pass failed");
+    double tot = 0;
+    for (auto x : q) tot += (double)x;
+    const char* nm[5] = {"tail/loop", "sample start + units", "node visits", "leaf primitives", "shading"};
+    for (int i = 0; i < 5; ++i) fprintf(stderr, "[world phase] %-22s %6.2f %%\n", nm[i], 100.0 * (double)q[i] / tot);
+  }
+#endif
   const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1);
   if (st != RTW_OK) return st;
   if (hipDeviceSynchronize() != hipSuccess) return rtw_fail(RTW_EHIP, "world counts pass failed");
