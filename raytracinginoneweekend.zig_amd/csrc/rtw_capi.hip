@@ -519,7 +519,7 @@ WsLayout ws_layout(const rtw_params* p) {
     const size_t segs = wf_segs(p), n = segs * rtwk::kSegCap;
     const size_t r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
     w.total += 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * 24) + 2 * al256(n * 4) +
-               2 * al256(segs * 4) + al256(segs * 8);
+               2 * al256(segs * 4) + al256(segs * 8) + al256(n * rtwk::kDrainWin * 24);
   }
   return w;
 }
@@ -604,6 +604,9 @@ struct WfLaunch<double> {
   static hipError_t fin(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_finish_f64(a, g, l, s, stats);
   }
+  static hipError_t drain(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_drain_f64(a, g, l, s, stats);
+  }
   static hipError_t gen_hit(const rtwk::WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
     return rtwk::launch_wf_generate_hit_f64(a, g, l, s);
   }
@@ -624,6 +627,9 @@ struct WfLaunch<float> {
   }
   static hipError_t fin(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
     return rtwk::launch_wf_finish_f32(a, g, l, s, stats);
+  }
+  static hipError_t drain(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+    return rtwk::launch_wf_drain_f32(a, g, l, s, stats);
   }
   static hipError_t gen_hit(const rtwk::WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s) {
     return rtwk::launch_wf_generate_hit_f32(a, g, l, s);
@@ -668,6 +674,7 @@ uint32_t* poll_words() {
 // batch behind, so the GPU never idles on the poll) left the queue empty, or
 // hands the drain to wf_finish once the live count shows retiring slots.
 // Empty batches cost only the launches: every wave reads its count first.
+constexpr uint32_t kWfBatch = 64;
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
 int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned char* ws, const WsLayout& L, int dev,
@@ -696,9 +703,14 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   uint32_t* seg_a = reinterpret_cast<uint32_t*>(take(segs * 4));
   uint32_t* seg_b = reinterpret_cast<uint32_t*>(take(segs * 4));
   a.seg_resv = reinterpret_cast<uint32_t*>(take(segs * 8));
+  a.drain_buf = reinterpret_cast<double*>(take(n * rtwk::kDrainWin * 24));
   a.live = reinterpret_cast<uint32_t*>(ws + L.live_off);
   a.n_slots = (uint32_t)n;
   a.n_segs = segs;
+  // Units per reservoir refill (RTW_WF_BATCH, default kWfBatch): the refills'
+  // atomics against the work a reservoir still holds when the queue runs dry.
+  const char* be = getenv("RTW_WF_BATCH");
+  a.batch = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
   // Persistent grids: every resident wave slot of each bounce kernel (at most
   // one wave per segment); the same grids for every launch of the frame.
   const uint32_t max_grid = (segs + rtwk::kTraceBlock / 64 - 1) / (rtwk::kTraceBlock / 64);
@@ -737,6 +749,10 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // the unit queue ran dry; 0 = drain through the queues to the end).
   const char* fe = getenv("RTW_WF_FINISH");
   const double fin_frac = (fe && *fe) ? atof(fe) : 1.0;
+  // Which in-register drain: wf_drain (samples dealt to the wave's free lanes,
+  // default) or wf_finish (RTW_WF_DRAIN=0: a lane runs its own slot's samples).
+  const char* de = getenv("RTW_WF_DRAIN");
+  const bool per_sample = !(de && *de == '0');
   int st = RTW_OK;
   for (uint64_t batch = 0;; ++batch) {
     for (int k = 0; k < kWfIters && st == RTW_OK; ++k) {
@@ -768,7 +784,8 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       if ((double)live < fin_frac * (double)n) {  // queue A holds the paths after this batch
         a.in = qa;
         a.seg_in = seg_a;
-        if ((e = WfLaunch<R>::fin(a, max_grid, lds, stream, stats)) != hipSuccess)
+        if ((e = per_sample ? WfLaunch<R>::drain(a, max_grid, lds, stream, stats)
+                                 : WfLaunch<R>::fin(a, max_grid, lds, stream, stats)) != hipSuccess)
           st = fail(RTW_EHIP, "wavefront finish launch: %s", hipGetErrorString(e));
         break;
       }

@@ -150,6 +150,7 @@ constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;
 // segment's reservoir (one global atomic per kWfBatch units), and a segment
 // runs on the same XCD every launch (fixed grid, round-robin dispatch).
 constexpr uint32_t kSegCap = 64;  // paths per segment (one 64-lane wave round)
+constexpr uint32_t kDrainWin = 32;  // wf_drain: samples of a unit dealt ahead of its fold (ring entries per slot)
 template <typename R>
 struct PathBuf {
   R *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz, *tm;
@@ -178,7 +179,9 @@ struct WfArgs {
   uint32_t* seg_out;   // [segment] live paths written to `out` (shade)
   uint32_t* seg_resv;  // [segment][2] unit reservoir [next, end)
   uint32_t* live;      // wf_count: sum of seg_in (host poll word)
+  double* drain_buf;   // wf_drain: [slot][kDrainWin][3] radiance of finished samples awaiting their fold
   uint32_t n_slots, n_segs;
+  uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
 };
 
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
@@ -189,6 +192,8 @@ hipError_t launch_wf_extend_f32(const WfArgs<float>& a, uint32_t grid, size_t ld
 hipError_t launch_wf_shade_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 hipError_t launch_wf_finish_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_wf_drain_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
+hipError_t launch_wf_drain_f32(const WfArgs<float>& a, uint32_t grid, size_t lds, hipStream_t s, bool stats);
 // Resident workgroups per CU of a bounce kernel (1 = extend, 2 = shade): the
 // persistent grid of that kernel is CUs x this.
 int wf_blocks_per_cu(int precision, int kernel, size_t lds);

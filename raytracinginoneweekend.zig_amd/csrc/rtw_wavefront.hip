@@ -29,7 +29,6 @@
 
 namespace rtwk {
 
-constexpr uint32_t kWfBatch = 64;  // units per reservoir refill (one global atomic)
 
 static_assert(offsetof(WfArgs<double>, t) == 0 && offsetof(WfArgs<float>, t) == 0,
               "kargs<R>() reads TraceArgs at kernarg offset 0");
@@ -75,13 +74,13 @@ __device__ __forceinline__ bool decode_unit(const TraceArgs<R>& A, uint32_t unit
 }
 
 // Lanes with `need` take units from the wave's reservoir [qnext, qend)
-// (wave-uniform), refilled kWfBatch units at a time from the device queue —
+// (wave-uniform), refilled `batch` units at a time from the device queue —
 // the megakernel's dealing (rtw_trace.hip step 1) with smaller batches, so
 // little work sits in reservoirs when the queue runs dry.  Wave-converged.  On return
 // `got` lanes own `unit`; lanes that found the queue exhausted do not.
 template <typename R>
-__device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, bool need, uint32_t lid, uint32_t& qnext,
-                                          uint32_t& qend, uint32_t& unit) {
+__device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, uint32_t batch, bool need, uint32_t lid,
+                                          uint32_t& qnext, uint32_t& qend, uint32_t& unit) {
   bool got = false;
   for (;;) {
     const uint64_t m = __ballot(need);
@@ -89,7 +88,7 @@ __device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, bool need, uint
     const uint32_t n = (uint32_t)__popcll(m);
     const uint32_t rank = mbcnt64(m);
     const uint32_t rem = qend - qnext;
-    const uint32_t grab = max(kWfBatch, n - rem);  // (used only when n > rem)
+    const uint32_t grab = max(batch, n - rem);  // (used only when n > rem)
     uint32_t base2 = 0;
     if (n > rem) {
       uint32_t b = 0;
@@ -188,12 +187,14 @@ __device__ __forceinline__ bool group_has_work(const WfArgs<R>& A) {
 // whether the lane holds a live path afterwards.  STATS: count finished
 // samples and shaded segments (rtw_render_counts); FIN: also as the
 // in-register drain's own counts (stats 9, 10: rtw_render_counts_ex).
-template <typename R, bool F32, bool STATS, bool FIN = false>
-__device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R>& T, uint32_t lid, bool valid,
-                                           Lane<R>& L, uint32_t slot, int hit, R tmax, uint32_t& qnext,
-                                           uint32_t& qend) {
-  const uint32_t npix = A.t.row_count * A.t.W;
-  bool ended = false, shading = false, miss = false;
+// The bounce of a lane's path (`valid`) on its closest hit: background on a
+// miss, else Material.scatter; `ended` when the sample is over (miss,
+// absorbed, or the depth bound).  Wave-converged (coop_reject).
+template <typename R, bool F32>
+__device__ __forceinline__ void bounce(const WfArgs<R>& A, const LdsTables<R>& T, uint32_t lid, bool valid, Lane<R>& L,
+                                       int hit, R tmax, bool& ended, bool& miss) {
+  bool shading = false;
+  ended = miss = false;
   uint32_t kind = 0;
   if (valid) {
     if (hit < 0) {  // miss: background (main.zig:109-112)
@@ -214,6 +215,15 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
     else if (L.depth == A.t.max_depth)
       ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
   }
+}
+
+template <typename R, bool F32, bool STATS, bool FIN = false>
+__device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R>& T, uint32_t lid, bool valid,
+                                           Lane<R>& L, uint32_t slot, int hit, R tmax, uint32_t& qnext,
+                                           uint32_t& qend) {
+  const uint32_t npix = A.t.row_count * A.t.W;
+  bool ended, miss;
+  bounce<R, F32>(A, T, lid, valid, L, hit, tmax, ended, miss);
   // A finished sample adds to its slot's chunk sum (main.zig:393).
   bool need_unit = false, need_sample = false;
   uint32_t unit = 0, s = 0;
@@ -242,7 +252,7 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
       need_sample = true;
     }
   }
-  if (take_unit(A.t, need_unit, lid, qnext, qend, unit)) {
+  if (take_unit(A.t, A.batch, need_unit, lid, qnext, qend, unit)) {
     uint32_t px, ly, c;
     decode_unit(A.t, unit, px, ly, c);
     s = c * A.t.chunk;
@@ -296,7 +306,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
     for (uint32_t k = 0; k < kSegCap; k += 64) {
       const uint32_t slot = base + k + lid;
       uint32_t unit = 0;
-      const bool got = take_unit(A.t, true, lid, qnext, qend, unit);
+      const bool got = take_unit(A.t, A.batch, true, lid, qnext, qend, unit);
       Lane<R> L{};
       if (got) {
         uint32_t px, ly, c;
@@ -523,6 +533,196 @@ __global__ void __launch_bounds__(kTraceBlock) wf_finish(WfArgs<R> A) {
   }
 }
 
+// ------------------------------------------------------------------- drain --
+// The drain dealt per SAMPLE (default; RTW_WF_DRAIN=0: wf_finish).  In
+// wf_finish a lane is its slot: it runs the rest of its unit's samples one
+// after another, so a wave lasts as long as its slowest slot (up to a whole
+// chunk of samples) while lanes whose slot retired idle — the drain ran at
+// about half the bounce kernels' segment rate.  Here the segment's slots only
+// OWN units (a row of `tab` in LDS, lane = slot): their remaining samples are
+// dealt to whichever lanes of the wave are free, so the wave stays full until
+// the segment's last samples.  A sample's radiance (T * background at a miss;
+// nothing for an absorbed or depth-bounded path) goes to a ring entry of its
+// unit (`drain_buf`, kDrainWin entries per slot), and the owner folds the
+// entries into the unit's f64 chunk sum strictly in sample order — the
+// addition sequence of every other engine, so the same bits.  At most
+// kDrainWin samples of a unit are dealt ahead of its fold (the ring's size).
+// A unit done publishes its chunk sum; its slot then takes the next unit from
+// the segment's reservoir / the device queue (retiring when there is none),
+// so the kernel is correct whenever it runs, as wf_finish.
+struct DrainUnit {  // 64 B per slot
+  uint32_t unit, next, end, fold;  // unit id, next sample to deal, sample end, next sample to fold
+  uint32_t ready, miss, live, pad; // ring bits (sample % kDrainWin): radiance stored / sample missed; unit held
+  double sum[3];                   // chunk sum of the folded samples
+  double pad2;
+};
+static_assert(sizeof(DrainUnit) == 64, "DrainUnit layout");
+
+template <typename R, bool F32, bool STATS>
+__global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  __shared__ DrainUnit tab_all[kTraceBlock / 64][kSegCap];
+  __shared__ uint32_t list_all[kTraceBlock / 64][64];
+  const uint32_t lid = lane_id();
+  // One wave per segment (the hardware dispatcher balances the waves; ordering
+  // the segments by the units their reservoirs hold, most first, measured
+  // equal: profiles/r03/wf_drain_ab.txt).
+  const uint32_t seg = wave_id();
+  const uint32_t n_in = seg < A.n_segs ? A.seg_in[seg] : 0u;
+  if (__syncthreads_or(n_in != 0u) == 0) return;
+  const SceneView<R> S = A.t.sc;
+  const LdsTables<R> T = stage_tables<R>(S, lds_raw);
+  const R tmin = A.t.tmin, pre_k = A.t.pre_k;
+  const uint32_t npix = A.t.row_count * A.t.W;
+  KStats st;
+  DrainUnit* tab = tab_all[threadIdx.x >> 6];
+  uint32_t* list = list_all[threadIdx.x >> 6];
+  static_assert(kSegCap == 64, "one slot per lane");
+  if (n_in != 0u) {  // (else every slot of the segment retired: no unit is left for it)
+    const uint32_t base = seg * kSegCap;
+    uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1];
+    tab[lid].live = 0u;  // a slot without a live path has retired
+    wave_lds_sync();
+    Lane<R> L{};
+    L.skip = -1;
+    uint32_t k = 0;  // the slot whose sample this lane traces
+    bool have = lid < n_in;
+    if (have) {  // the in-flight sample of slot k, from queue A
+      uint32_t slot;
+      load_path(A.in, base + lid, L, slot);
+      k = slot - base;
+      const uint32_t unit = A.home_unit[slot], s = A.home_s[slot];
+      uint32_t px, ly, c;
+      decode_unit(A.t, unit, px, ly, c);
+      L.s = s;
+      DrainUnit& u = tab[k];
+      u.unit = unit;
+      u.next = s + 1u;
+      u.end = chunk_end(A.t, c);
+      u.fold = s;
+      u.ready = u.miss = 0u;
+      u.live = 1u;
+      const double* hs = A.home_sum + 3 * (size_t)slot;
+      u.sum[0] = hs[0], u.sum[1] = hs[1], u.sum[2] = hs[2];
+    }
+    wave_lds_sync();
+    for (;;) {
+      // 1. Deal: each pass gives every free lane one sample of a unit with
+      // samples left in its window (the offering units in slot order).
+      bool fresh = false;
+      uint32_t fu = 0, fs = 0;
+      for (;;) {
+        const uint64_t needm = wballot(!have);
+        if (!needm) break;
+        const uint32_t o_next = tab[lid].next, o_end = tab[lid].end, o_fold = tab[lid].fold;
+        const bool offer = tab[lid].live != 0u && o_next < min(o_end, o_fold + kDrainWin);
+        const uint64_t offm = wballot(offer);
+        if (!offm) break;
+        const uint32_t nn = popc64(needm), ro = mbcnt64(offm);
+        if (offer) {
+          list[ro] = lid;
+          if (ro < nn) tab[lid].next = o_next + 1u;  // its sample o_next is dealt now
+        }
+        wave_lds_sync();
+        const uint32_t rw = mbcnt64(needm);
+        if (!have && rw < popc64(offm)) {
+          k = list[rw];
+          fu = tab[k].unit;
+          fs = tab[k].next - 1u;
+          fresh = have = true;
+        }
+        wave_lds_sync();
+      }
+      if (!wany(have)) break;  // nothing in flight, nothing left to deal
+      if (fresh) start_path(A.t, fu, fs, L);
+      // 2. One segment of every lane's path.
+      int hit = -1;
+      R tmax = (R)__builtin_huge_val();
+      if (have) closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+      bool ended, miss;
+      bounce<R, F32>(A, T, lid, have, L, hit, tmax, ended, miss);
+      if constexpr (STATS) {
+        const uint32_t ns = popc64(wballot(ended)), nv = popc64(wballot(have));
+        if (lid == 0) {
+          atomicAdd(A.t.stats + 0, (unsigned long long)ns);
+          atomicAdd(A.t.stats + 1, (unsigned long long)nv);
+          atomicAdd(A.t.stats + 9, (unsigned long long)nv);
+          atomicAdd(A.t.stats + 10, (unsigned long long)ns);
+        }
+      }
+      // 3. A finished sample's radiance goes to its unit's ring entry.
+      if (ended) {
+        const uint32_t bit = 1u << (L.s % kDrainWin);
+        if (miss) {
+          const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
+          double* b = A.drain_buf + ((size_t)(base + k) * kDrainWin + L.s % kDrainWin) * 3;
+          b[0] = (double)col.x;
+          b[1] = (double)col.y;
+          b[2] = (double)col.z;
+          atomicOr(&tab[k].miss, bit);
+        }
+        atomicOr(&tab[k].ready, bit);
+        have = false;
+      }
+      // the ring entries written above are read by other lanes of this wave
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      // 4. Owners fold their ready samples in sample order (main.zig:393); a
+      // unit done publishes its chunk sum and the slot takes the next unit.
+      bool need_unit = false;
+      if (tab[lid].live) {
+        uint32_t fold = tab[lid].fold, ready = tab[lid].ready;
+        const uint32_t mm = tab[lid].miss, end = tab[lid].end;
+        double sx = tab[lid].sum[0], sy = tab[lid].sum[1], sz = tab[lid].sum[2];
+        while ((ready >> (fold % kDrainWin)) & 1u) {
+          const uint32_t j = fold % kDrainWin;
+          if ((mm >> j) & 1u) {  // only a miss adds (the other engines' `sx += col`)
+            const double* b = A.drain_buf + ((size_t)(base + lid) * kDrainWin + j) * 3;
+            sx += b[0];
+            sy += b[1];
+            sz += b[2];
+          }
+          ready &= ~(1u << j);
+          ++fold;
+        }
+        tab[lid].fold = fold;
+        tab[lid].ready = ready;
+        tab[lid].miss = mm & ready;  // bits of folded samples cleared with their ready bits
+        tab[lid].sum[0] = sx, tab[lid].sum[1] = sy, tab[lid].sum[2] = sz;
+        if (fold == end) {
+          uint32_t px, ly, c;
+          decode_unit(A.t, tab[lid].unit, px, ly, c);
+          double* dst = A.t.partial + ((size_t)c * npix + (size_t)ly * A.t.W + px) * 3;
+          dst[0] = sx;
+          dst[1] = sy;
+          dst[2] = sz;
+          tab[lid].live = 0u;
+          need_unit = true;
+        }
+      }
+      uint32_t unit = 0;
+      if (take_unit(A.t, A.batch, need_unit, lid, qnext, qend, unit)) {
+        uint32_t px, ly, c;
+        decode_unit(A.t, unit, px, ly, c);
+        DrainUnit& u = tab[lid];
+        u.unit = unit;
+        u.next = u.fold = c * A.t.chunk;
+        u.end = chunk_end(A.t, c);
+        u.ready = u.miss = 0u;
+        u.live = 1u;
+        u.sum[0] = u.sum[1] = u.sum[2] = 0.0;
+      }
+      wave_lds_sync();
+    }
+    if (lid == 0) {
+      A.seg_in[seg] = 0u;
+      A.seg_resv[2 * seg] = qnext;
+      A.seg_resv[2 * seg + 1] = qend;
+    }
+  }
+}
+
 // Live paths of a queue = sum of its segment counts (the host's poll word).
 __global__ void __launch_bounds__(1024) wf_count(const uint32_t* seg, uint32_t n, uint32_t* live) {
   __shared__ uint32_t part[16];
@@ -583,6 +783,10 @@ static hipError_t launch3(int k, const WfArgs<R>& a, uint32_t grid, size_t lds, 
     hipLaunchKernelGGL((wf_shade<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (k == 3)
     hipLaunchKernelGGL((wf_shade<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 9)
+    hipLaunchKernelGGL((wf_drain<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
+  else if (k == 10)
+    hipLaunchKernelGGL((wf_drain<R, F32, true>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else if (k == 4)
     hipLaunchKernelGGL((wf_finish<R, F32, false>), dim3(grid), dim3(kTraceBlock), lds, s, a);
   else
@@ -603,6 +807,12 @@ hipError_t launch_wf_finish_f64(const WfArgs<double>& a, uint32_t g, size_t l, h
 }
 hipError_t launch_wf_finish_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
   return launch3<float, true>(stats ? 5 : 4, a, g, l, s);
+}
+hipError_t launch_wf_drain_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<double, false>(stats ? 10 : 9, a, g, l, s);
+}
+hipError_t launch_wf_drain_f32(const WfArgs<float>& a, uint32_t g, size_t l, hipStream_t s, bool stats) {
+  return launch3<float, true>(stats ? 10 : 9, a, g, l, s);
 }
 hipError_t launch_wf_generate_hit_f64(const WfArgs<double>& a, uint32_t g, size_t l, hipStream_t s) {
   return launch3<double, false>(6, a, g, l, s);

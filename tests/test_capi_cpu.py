@@ -111,13 +111,14 @@ def test_workspace_bytes(rtw):
 
 def test_workspace_bytes_wavefront(rtw):
     """Wavefront engine: + two SoA path queues (each with the fused engine's
-    hit root / winner per path), the split engine's hit arrays and the home
-    slots (rtw_capi.hip ws_layout) per in-flight path, + per-segment words."""
+    hit root / winner per path), the split engine's hit arrays, the home
+    slots and wf_drain's ring of 32 f64x3 sample radiances (rtw_capi.hip
+    ws_layout) per in-flight path, + per-segment words."""
     base = rtw.workspace_bytes(rtw.make_params(1200, 675, 500))
     for prec, r in (("f64", 8), ("f32", 4)):
         for n in (1 << 16, 1 << 20):
             p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n)
-            per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + (24 + 4 + 4)  # queues carry the fused hit
+            per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + (24 + 4 + 4) + 32 * 24  # queues carry the fused hit
             segs = n // 64  # one 64-path queue segment: 2 counts + a unit reservoir
             extra = rtw.workspace_bytes(p) - base
             assert n * per_path + segs * 16 <= extra <= n * per_path + segs * 16 + 64 * 256

@@ -1,7 +1,8 @@
 """GPU parity of the wavefront engine (BASELINE.json configs[3]: SoA path
 queues in HBM, per-bounce kernels — fused shade + closest hit, or separate
-extend / shade — persistent grids, and the in-register drain wf_finish once
-slots retire).
+extend / shade — persistent grids, and an in-register drain once slots
+retire: wf_drain, the remaining samples dealt to the wave's free lanes and
+folded in sample order, or wf_finish, a lane per slot).
 
 It computes the same Tier-B image as the megakernel: every sample runs the
 same device functions in the same order and a home slot adds its unit's
@@ -19,12 +20,14 @@ from test_gpu_parity import ASPECT, assert_parity, custom_scene, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["finish", "queues"])
+@pytest.fixture(autouse=True, params=["samples", "finish", "queues"])
 def drain(request, monkeypatch):
-    """Every test runs with both drains: wf_finish in registers once slots
-    retire (the default) and the bounce kernels' queues to the end
-    (RTW_WF_FINISH=0, read by the library on every render)."""
-    monkeypatch.setenv("RTW_WF_FINISH", "1" if request.param == "finish" else "0")
+    """Every test runs with the three drains: in registers once slots retire,
+    by wf_drain (samples dealt to free lanes, the default) or wf_finish
+    (RTW_WF_DRAIN=0), and the bounce kernels' queues to the end
+    (RTW_WF_FINISH=0); read by the library on every render."""
+    monkeypatch.setenv("RTW_WF_FINISH", "0" if request.param == "queues" else "1")
+    monkeypatch.setenv("RTW_WF_DRAIN", "0" if request.param == "finish" else "1")
     return request.param
 
 
