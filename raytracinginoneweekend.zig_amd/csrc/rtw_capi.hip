@@ -524,6 +524,16 @@ WsLayout ws_layout(const rtw_params* p) {
   return w;
 }
 
+// Unit dealing order (rtw_device.hpp dealt_unit): RTW_UNIT_ORDER=fwd|rev
+// overrides the engine's default.
+uint32_t unit_order(uint32_t dflt) {
+  const char* uo = getenv("RTW_UNIT_ORDER");
+  if (uo && std::strcmp(uo, "fwd") == 0) return 0u;
+  if (uo && std::strcmp(uo, "rev") == 0) return 1u;
+  return dflt;
+}
+constexpr uint32_t kWorldUnitOrder = 1u;
+
 template <typename R>
 void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_camera* cam, const rtw_params* p,
                unsigned char* ws, const WsLayout& L) {
@@ -563,6 +573,11 @@ void fill_args(rtwk::TraceArgs<R>& a, const rtwk::SceneView<R>& v, const rtw_cam
   const rtwm::UDivMagic mu = rtwm::udiv_magic(rtwk::kTileW * rtwk::kTileH * a.n_chunks), mt = rtwm::udiv_magic(a.tiles_x);
   a.upt_m = mu.m, a.upt_sh = mu.sh, a.tx_m = mt.m, a.tx_sh = mt.sh;
   a.seed_base = splitmix_first(p->seed);
+  // Unit dealing order (rtw_device.hpp dealt_unit): image order, top rows
+  // first, for the cover-scene engines, last-first for the world kernel
+  // (rtw_fill_trace_args), each the faster in the in-process A/Bs
+  // (profiles/r03/unit_order_ab.txt); RTW_UNIT_ORDER=fwd|rev overrides.
+  a.unit_order = unit_order(0u);
   a.partial = reinterpret_cast<double*>(ws + L.partial_off);
   a.counter = reinterpret_cast<uint32_t*>(ws + L.counter_off);
   a.stats = reinterpret_cast<unsigned long long*>(ws + L.stats_off);
@@ -1056,6 +1071,7 @@ size_t rtw_ws_counter_off(const rtw_params* p) { return ws_layout(p).counter_off
 int rtw_device_cus(int dev) { return device_cus(dev); }
 void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, const rtw_params* p, unsigned char* ws) {
   fill_args(a, rtwk::SceneView<double>{}, cam, p, ws, ws_layout(p));
+  a.unit_order = unit_order(kWorldUnitOrder);  // the world kernel's default (fill_args)
 }
 int rtw_launch_finalize(const rtw_params* p, unsigned char* ws, uint8_t* d_rgb, float* d_mean, hipStream_t s) {
   const WsLayout L = ws_layout(p);

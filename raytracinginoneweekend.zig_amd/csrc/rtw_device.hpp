@@ -101,6 +101,18 @@ __device__ __forceinline__ R sqrt_k(R x) {
     return sqrt(x);
 }
 
+// ------------------------------------------------------------- work units --
+// The unit a work-queue index deals.  Unit ids run over 8x8 pixel tiles in
+// image-row order, top rows first, each tile's chunks in order (one 64-unit
+// batch = one (tile, chunk)); order 1 deals them last-first.  Which lane runs
+// a unit, and when, changes no bit of its chunk sum; the order moves which
+// units run together and which end the launch (measured per engine:
+// rtw_capi.hip fill_args, profiles/r03/unit_order_ab.txt).
+template <typename A>
+__device__ __forceinline__ uint32_t dealt_unit(uint32_t raw, const A& a) {
+  return a.unit_order ? a.total_units - 1u - raw : raw;
+}
+
 // ------------------------------------------------------------------ RNG --
 // Counter-based Zig std.Random.SplitMix64: sample (pixel p, sample s) owns the
 // 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its

@@ -84,7 +84,7 @@ struct TraceArgs {
   uint32_t row_begin, row_stride, row_count, tiles_x;
   uint32_t total_units;
   uint32_t upt_m, upt_sh, tx_m, tx_sh;  // rtwm::udiv magic of units per tile (64 * n_chunks) and tiles_x
-  uint32_t pad;
+  uint32_t unit_order;            // rtw_device.hpp dealt_unit: 0 image order, 1 last-first
   uint64_t seed_base;             // SplitMix64(seed).next()
   double* partial;                // [n_chunks][row_count*W][3] chunk sums
   uint32_t* counter;              // work-queue head (zeroed before launch)

@@ -119,7 +119,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if constexpr ((VAR & kVarBatchDecode) != 0) {
         // A batch is 64 aligned units = one (tile, chunk): decoded once per
         // batch (wave-uniform) instead of two integer divisions per refill.
-        if (n > rem) decode_batch(base2, nb_tx, nb_ty, nb_c);
+        if (n > rem)  // (a dealt batch is a 64-aligned batch in every order)
+          decode_batch(dealt_unit(base2, *opaque(kargs<R>())) & ~63u, nb_tx, nb_ty, nb_c);
       }
       if (need) {
         const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
@@ -127,7 +128,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
           done = true;
         } else {
           uint32_t tx, ty, c;
-          const uint32_t l = unit & 63u;
+          const uint32_t du = dealt_unit(unit, *opaque(kargs<R>()));
+          const uint32_t l = du & 63u;
           if constexpr ((VAR & kVarBatchDecode) != 0) {
             const bool in_cur = rank < rem;
             tx = in_cur ? cur_tx : nb_tx;
@@ -135,8 +137,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
             c = in_cur ? cur_c : nb_c;
           } else {
             const uint32_t units_per_tile = kTileW * kTileH * RTW_KA(n_chunks);
-            const uint32_t tile = rtwm::udiv(unit, RTW_KA(upt_m), RTW_KA(upt_sh));  // unit / units_per_tile
-            const uint32_t r = unit - tile * units_per_tile;
+            const uint32_t tile = rtwm::udiv(du, RTW_KA(upt_m), RTW_KA(upt_sh));  // du / units_per_tile
+            const uint32_t r = du - tile * units_per_tile;
             c = r >> 6;
             ty = rtwm::udiv(tile, RTW_KA(tx_m), RTW_KA(tx_sh));  // tile / tiles_x
             tx = tile - ty * RTW_KA(tiles_x);

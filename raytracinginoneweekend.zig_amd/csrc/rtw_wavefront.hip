@@ -96,14 +96,17 @@ __device__ __forceinline__ bool take_unit(const TraceArgs<R>& A, uint32_t batch,
       base2 = __shfl(b, 0);
     }
     if (need) {
-      const uint32_t u = rank < rem ? qnext + rank : base2 + (rank - rem);
+      const uint32_t raw = rank < rem ? qnext + rank : base2 + (rank - rem);
       uint32_t px, ly, c;
-      if (u >= A.total_units) {
+      if (raw >= A.total_units) {
         need = false;  // queue exhausted: the slot retires
-      } else if (decode_unit(A, u, px, ly, c)) {
-        need = false;
-        got = true;
-        unit = u;
+      } else {
+        const uint32_t u = dealt_unit(raw, A);
+        if (decode_unit(A, u, px, ly, c)) {
+          need = false;
+          got = true;
+          unit = u;
+        }
       }
     }
     if (n > rem) {

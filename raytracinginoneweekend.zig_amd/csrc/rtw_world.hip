@@ -527,10 +527,11 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         base2 = __shfl(b, 0);
       }
       if (need) {
-        const uint32_t unit = rank < rem ? qnext + rank : base2 + (rank - rem);
-        if (unit >= WKA(t.total_units)) {
+        const uint32_t raw = rank < rem ? qnext + rank : base2 + (rank - rem);
+        if (raw >= WKA(t.total_units)) {
           done = true;
         } else {
+          const uint32_t unit = dealt_unit(raw, WKA(t));
           const uint32_t units_per_tile = kTileW * kTileH * WKA(t.n_chunks);
           const uint32_t tile = rtwm::udiv(unit, WKA(t.upt_m), WKA(t.upt_sh));  // unit / units_per_tile
           const uint32_t r = unit - tile * units_per_tile;

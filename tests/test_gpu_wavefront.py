@@ -158,4 +158,9 @@ def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, d
     if drain == "queues":
         assert wf["drain_segments"] == wf["drain_samples"] == 0
     else:
-        assert 0 < wf["drain_segments"] < wf["segments"] and 0 < wf["drain_samples"] < wf["samples"]
+        assert wf["drain_segments"] < wf["segments"] and wf["drain_samples"] < wf["samples"]
+        # (one 64-path segment on the sky units the queue deals last: every
+        # slot's last unit ends in the same bounce, so no poll sees slots
+        # retiring and the drain may not run at all)
+        if paths != 64:
+            assert wf["drain_segments"] > 0 and wf["drain_samples"] > 0

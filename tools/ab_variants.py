@@ -1,5 +1,7 @@
 """In-process A/B of trace-kernel tuning variants (RTW_VARIANT), interleaved
-rounds on one device (guide §5.4 rule 24).  Usage: ab_variants.py prec v1,v2,... [rounds]"""
+rounds on one device (guide §5.4 rule 24).  Usage: ab_variants.py prec v1,v2,... [rounds]
+An item may carry environment settings read by the library at each render:
+"0:RTW_UNIT_ORDER=fwd" (several joined by '+')."""
 import os
 import sys
 import time
@@ -12,7 +14,7 @@ import rtw_amd as R  # noqa: E402
 from rtw_amd.device import TorchRenderer  # noqa: E402
 
 prec = sys.argv[1] if len(sys.argv) > 1 else "f64"
-variants = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "0").split(",")]
+variants = (sys.argv[2] if len(sys.argv) > 2 else "0").split(",")
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 W, spp = 1200, 500
 H = R.image_height(W, 16 / 9)
@@ -25,7 +27,10 @@ res = {v: [] for v in variants}
 timer = R.Timer()
 for r in range(rounds + 1):
     for v in variants:
-        os.environ["RTW_VARIANT"] = str(v)
+        var, _, envs = v.partition(":")
+        for kv in [e for e in envs.split("+") if e]:
+            os.environ[kv.split("=")[0]] = kv.split("=", 1)[1]
+        os.environ["RTW_VARIANT"] = var
         img = rend.render(cam, p, timer=timer)
         ms = timer.elapsed_ms()
         if r == 0:  # warmup + equality check
@@ -35,6 +40,8 @@ for r in range(rounds + 1):
             assert torch.equal(a, ref), f"variant {v} changed the image"
             continue
         res[v].append(ms)
+        for kv in [e for e in envs.split("+") if e]:
+            os.environ.pop(kv.split("=")[0], None)
 for v in variants:
     xs = sorted(res[v])
     print(f"{prec} var {v}: median {xs[len(xs)//2]:.3f} ms  min {xs[0]:.3f}  -> {W*H*spp/xs[len(xs)//2]/1e3:.0f} Msamples/s",
