@@ -264,7 +264,10 @@ struct WorldArgs {
   WorldView w;
   double margin;        // BVH test widening (rtw_world_capi.hip bvh_margin)
   unsigned long long* counts;  // stats pass: {samples, segments, node visits, prim tests}
+  double* ring;         // tail dealing: [lane of the grid][kTailWin][3] radiance of samples traced for that lane's unit
+  uint32_t tail_deal;   // 1: lanes the queue left without a unit trace samples of the wave's other units
 };
+constexpr uint32_t kTailWin = 32;  // world kernel: the last samples of a unit other lanes may trace (ring entries)
 
 // occ: register-allocation target (workgroups per CU): 1 (none), 3 or 4.
 // fs: the kernel's feature set, world_feature_set(features of the world):

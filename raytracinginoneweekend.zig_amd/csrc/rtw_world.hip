@@ -485,6 +485,18 @@ template <int MODE, int OCC, int FEAT>
 __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kBvhStack;  // this wave's stack
+  // Tail dealing rows of this wave's lanes (lane = the owner of a unit): the
+  // first sample handed to other lanes (samples [hi, s_end) are theirs), the
+  // ring entries they filled, the unit's pixel; and the dealing list.
+  // (Row addresses formed at each use from the wave-uniform index: held as
+  // pointers they cost registers across the whole loop.)
+  __shared__ uint32_t tail_rows[kWorldBlock / 64][5][64];
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#define TL_HI tail_rows[wv][0]
+#define TL_READY tail_rows[wv][1]
+#define TL_PXLY tail_rows[wv][2]
+#define TL_LIST tail_rows[wv][3]
+#define TL_OWN tail_rows[wv][4]  // a helper's owner lane
   // The world's fields are re-read from the kernel argument where used
   // (scalar loads through a laundered kernarg pointer) instead of living in
   // SGPRs for the whole kernel: at the 100-SGPR limit they spill to VGPR
@@ -508,11 +520,14 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // so that one term joins the chunk sum directly: sx + (0 + x) == sx + x
   // (x >= +0), the oracle's `rad` (rtw_world.c sample_b) without its registers.
   bool have_unit = false, have_ray = false, done = false;
+  bool waiting = false;  // owner: its own samples done, waiting for the ones other lanes trace
+  bool helping = false;  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
   uint32_t qnext = 0, qend = 0;
-  unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0;
+  unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
   KStats st;  // MODE 2: phase stamps
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
   for (;;) {
+    if (MODE == 1) ++n_iters;  // wave iterations (lane utilisation = segments / (64 x iterations))
     // ---- take units (wave-uniform; rtw_trace.hip step 1) ----
     const bool need = !have_unit && !done;
     const uint64_t needmask = __ballot(need);
@@ -546,6 +561,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
             L.s = L.c * WKA(t.chunk);
             L.s_end = min(L.s + WKA(t.chunk), WKA(t.spp));
             L.sx = L.sy = L.sz = 0.0;
+            TL_HI[lid] = L.s_end;
+            TL_READY[lid] = 0u;
+            TL_PXLY[lid] = px | (ly << 16);
           }
         }
       }
@@ -560,8 +578,50 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       if (__all(done)) break;
       continue;
     }
+    // ---- tail: once the queue ran dry for some lane of the wave, the lanes
+    // left without a unit trace the LAST samples of the wave's other units
+    // (one per offering unit per pass, up to kTailWin of a unit), each
+    // sample's radiance going to its owner's ring; an owner stops at the
+    // first sample it handed out and folds the ring in sample order
+    // (main.zig:393), the other engines' addition sequence.  A world unit
+    // runs ~84 wave iterations, so without this the launch ends with lanes
+    // idle while the last units finish.
+    const bool tail = WKA(tail_deal) != 0u && __any(done);
+    if (tail) {
+      for (;;) {
+        const bool free_lane = done && !have_unit && !helping;
+        const uint64_t needm = wballot(free_lane);
+        if (!needm) break;
+        uint32_t hi = 0;
+        bool offer = false;
+        if (have_unit && !waiting) {  // (L.s: the sample in flight or the next to start)
+          hi = TL_HI[lid];
+          offer = hi > max(L.s + 1u, L.s_end > kTailWin ? L.s_end - kTailWin : 0u);
+        }
+        const uint64_t offm = wballot(offer);
+        if (!offm) break;
+        const uint32_t ro = mbcnt64(offm);
+        if (offer) {
+          TL_LIST[ro] = lid | ((hi - 1u) << 6);
+          if (ro < popc64(needm)) TL_HI[lid] = hi - 1u;
+        }
+        wave_lds_sync();
+        const uint32_t rw = mbcnt64(needm);
+        if (free_lane && rw < popc64(offm)) {
+          const uint32_t e = TL_LIST[rw];
+          helping = true;
+          TL_OWN[lid] = e & 63u;
+          L.s = e >> 6;
+          const uint32_t pl = TL_PXLY[e & 63u];
+          L.px = pl & 0xFFFFu;
+          L.ly = pl >> 16;
+          L.sx = L.sy = L.sz = 0.0;
+        }
+        wave_lds_sync();
+      }
+    }
     // ---- new sample ----
-    if (have_unit && !have_ray) {
+    if (((have_unit && !waiting) || helping) && !have_ray) {
       D u, v, dk[2];
       start_sample_uv<D>(kargs<D>(), L, u, v);
       for (;;) {  // randomPointInUnitDisk, rand.zig:30-36
@@ -704,10 +764,21 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       }
     }
     WSTAMP(4)  // hit record, texture, scatter (+ the NaN fallback)
-    if (ended) {  // (its radiance joined the chunk sum above, main.zig:393)
+    if (ended && helping) {  // a sample of another lane's unit: its radiance to that lane's ring
+      const uint32_t j = L.s % kTailWin, o = TL_OWN[lid];
+      double* rg = WKA(ring) + ((size_t)(blockIdx.x * kWorldBlock + wv * 64u + o) * kTailWin + j) * 3;
+      rg[0] = L.sx;
+      rg[1] = L.sy;
+      rg[2] = L.sz;
+      atomicOr(&TL_READY[o], 1u << j);
+      helping = false;
+      have_ray = false;
+      if (MODE == 1) ++n_samples;
+    } else if (ended) {  // (its radiance joined the chunk sum above, main.zig:393)
       L.s++;
       have_ray = false;
       if (MODE == 1) ++n_samples;
+      if (L.s != L.s_end && tail && L.s == TL_HI[lid]) waiting = true;  // the rest went to other lanes
       if (L.s == L.s_end) {
         const uint32_t npix = WKA(t.row_count) * WKA(t.W);
         double* dst = WKA(t.partial) + ((size_t)L.c * npix + (size_t)L.ly * WKA(t.W) + L.px) * 3;
@@ -717,7 +788,40 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         have_unit = false;
       }
     }
+    // ---- owners waiting on other lanes' samples fold their ring in order ----
+    if (tail) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the ring entries written above
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (waiting) {
+        uint32_t rdy = TL_READY[lid];
+        const double* rb = WKA(ring) + (size_t)(blockIdx.x * kWorldBlock + threadIdx.x) * kTailWin * 3;
+        while (L.s != L.s_end && ((rdy >> (L.s % kTailWin)) & 1u)) {
+          const uint32_t j = L.s % kTailWin;
+          L.sx += rb[3 * j];
+          L.sy += rb[3 * j + 1];
+          L.sz += rb[3 * j + 2];
+          rdy &= ~(1u << j);
+          L.s++;
+        }
+        TL_READY[lid] = rdy;
+        if (L.s == L.s_end) {
+          const uint32_t npix = WKA(t.row_count) * WKA(t.W);
+          double* dst = WKA(t.partial) + ((size_t)L.c * npix + (size_t)L.ly * WKA(t.W) + L.px) * 3;
+          dst[0] = L.sx;
+          dst[1] = L.sy;
+          dst[2] = L.sz;
+          have_unit = false;
+          waiting = false;
+        }
+      }
+    }
   }
+#undef TL_HI
+#undef TL_READY
+#undef TL_PXLY
+#undef TL_LIST
+#undef TL_OWN
   if constexpr (MODE == 2) {
     WSTAMP(0)
     if (lid == 0)
@@ -728,6 +832,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     atomicAdd(A.counts + 1, n_segments);
     atomicAdd(A.counts + 2, n_visits);
     atomicAdd(A.counts + 3, n_tests);
+    if (lid == 0) atomicAdd(A.counts + 4, n_iters);
   }
 }
 

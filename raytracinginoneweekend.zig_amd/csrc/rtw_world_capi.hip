@@ -240,6 +240,8 @@ struct rtw_world_s {
   bool has_moving = false;
   uint32_t feat = 0;  // features used (rtw_world.hip kFeat*): picks the kernel instantiation
   uint32_t info[4] = {0, 0, 0, 0};
+  void* ring = nullptr;  // tail dealing's per-lane rings (WorldArgs::ring), grown to the largest grid launched
+  size_t ring_bytes = 0;
 };
 
 extern "C" {
@@ -504,6 +506,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
 int rtw_world_destroy(rtw_world w) {
   if (!w) return RTW_OK;
   if (w->buf) (void)hipFree(w->buf);
+  if (w->ring) (void)hipFree(w->ring);
   delete w;
   return RTW_OK;
 }
@@ -588,6 +591,19 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   const int bpc = bpc_cache[fs][oi];
   const uint32_t want = (a.t.total_units + 255) / 256;
   const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
+  // Tail dealing (default; RTW_WORLD_TAIL=0: off): the rings of the grid's lanes.
+  const char* te = getenv("RTW_WORLD_TAIL");
+  a.tail_deal = (te && *te == '0') ? 0u : 1u;
+  const size_t ring_need = (size_t)grid * rtwk::kWorldBlock * rtwk::kTailWin * 3 * sizeof(double);
+  if (a.tail_deal && w->ring_bytes < ring_need) {
+    if (w->ring && (hipStreamSynchronize(stream) != hipSuccess || hipFree(w->ring) != hipSuccess))
+      return rtw_fail(RTW_EHIP, "tail ring release failed");
+    w->ring = nullptr;
+    w->ring_bytes = 0;
+    if (hipMalloc(&w->ring, ring_need) != hipSuccess) return rtw_fail(RTW_EHIP, "tail ring: hipMalloc(%zu) failed", ring_need);
+    w->ring_bytes = ring_need;
+  }
+  a.ring = static_cast<double*>(w->ring);
   if (timer && rtw_timer_mark(timer, stream, true) != RTW_OK) return RTW_EHIP;
   hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode, oi, fs);
   if (e != hipSuccess) return rtw_fail(RTW_EHIP, "world kernel launch: %s", hipGetErrorString(e));
@@ -630,11 +646,14 @@ int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params
   const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1);
   if (st != RTW_OK) return st;
   if (hipDeviceSynchronize() != hipSuccess) return rtw_fail(RTW_EHIP, "world counts pass failed");
-  unsigned long long c[4];
+  unsigned long long c[5];
   if (hipMemcpy(c, static_cast<unsigned char*>(ws) + rtw_ws_stats_off(p), sizeof(c), hipMemcpyDeviceToHost) !=
       hipSuccess)
     return rtw_fail(RTW_EHIP, "counts copy failed");
   for (int i = 0; i < 4; ++i) counts_out[i] = c[i];
+  if (const char* v = getenv("RTW_COUNTS_VERBOSE"); v && *v == '1')  // diagnostic: lanes busy per wave iteration
+    fprintf(stderr, "[world counts] wave iterations %llu, segments per wave iteration %.2f of 64\n", c[4],
+            (double)c[1] / (double)(c[4] ? c[4] : 1));
   return RTW_OK;
 }
 
