@@ -23,6 +23,8 @@
 // miss).  oracle/rtw_world.h Tier B is the written contract.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rtw_device.hpp"
 #include "rtw_libm.hpp"
 
@@ -526,7 +528,12 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
   KStats st;  // MODE 2: phase stamps
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
-  for (;;) {
+  // The loop body, compiled twice: without the tail dealing for the bulk of
+  // the launch, and with it once the queue ran dry for some lane of the wave
+  // (its variables then are not live in the bulk loop's register allocation).
+  // Returns 1 when every lane is done.
+  auto body = [&](auto tail_tag) -> int {
+    constexpr bool TAIL = decltype(tail_tag)::value;
     if (MODE == 1) ++n_iters;  // wave iterations (lane utilisation = segments / (64 x iterations))
     // ---- take units (wave-uniform; rtw_trace.hip step 1) ----
     const bool need = !have_unit && !done;
@@ -575,8 +582,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       }
     }
     if (!__any(have_unit)) {
-      if (__all(done)) break;
-      continue;
+      if (__all(done)) return 1;
+      return 0;
     }
     // ---- tail: once the queue ran dry for some lane of the wave, the lanes
     // left without a unit trace the LAST samples of the wave's other units
@@ -586,8 +593,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     // (main.zig:393), the other engines' addition sequence.  A world unit
     // runs ~84 wave iterations, so without this the launch ends with lanes
     // idle while the last units finish.
-    const bool tail = WKA(tail_deal) != 0u && __any(done);
-    if (tail) {
+    constexpr bool tail = TAIL;
+    if constexpr (tail) {
       for (;;) {
         const bool free_lane = done && !have_unit && !helping;
         const uint64_t needm = wballot(free_lane);
@@ -789,7 +796,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       }
     }
     // ---- owners waiting on other lanes' samples fold their ring in order ----
-    if (tail) {
+    if constexpr (tail) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the ring entries written above
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -815,6 +822,15 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           waiting = false;
         }
       }
+    }
+    return 0;
+  };
+  for (;;) {
+    if (body(std::false_type{}) == 1) break;
+    if (WKA(tail_deal) != 0u && __any(done)) {
+      while (body(std::true_type{}) != 1) {
+      }
+      break;
     }
   }
 #undef TL_HI
