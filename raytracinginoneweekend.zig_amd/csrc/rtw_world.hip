@@ -492,13 +492,16 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // ring entries they filled, the unit's pixel; and the dealing list.
   // (Row addresses formed at each use from the wave-uniform index: held as
   // pointers they cost registers across the whole loop.)
-  __shared__ uint32_t tail_rows[kWorldBlock / 64][5][64];
+  __shared__ uint32_t tail_rows[kWorldBlock / 64][6][64];
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #define TL_HI tail_rows[wv][0]
 #define TL_READY tail_rows[wv][1]
 #define TL_PXLY tail_rows[wv][2]
 #define TL_LIST tail_rows[wv][3]
 #define TL_OWN tail_rows[wv][4]  // a helper's owner lane
+#define TL_C tail_rows[wv][5]    // the unit's chunk
+  // (The unit's pixel and chunk live only in these rows, read where used —
+  // sample start, chunk-sum publish — instead of VGPRs across the loop.)
   // The world's fields are re-read from the kernel argument where used
   // (scalar loads through a laundered kernarg pointer) instead of living in
   // SGPRs for the whole kernel: at the 100-SGPR limit they spill to VGPR
@@ -562,10 +565,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           const uint32_t px = tx * kTileW + ((r & 63u) & 7u), ly = ty * kTileH + ((r & 63u) >> 3);
           if (px < WKA(t.W) && ly < WKA(t.row_count)) {
             have_unit = true;
-            L.px = px;
-            L.ly = ly;
-            L.c = r >> 6;
-            L.s = L.c * WKA(t.chunk);
+            L.s = (r >> 6) * WKA(t.chunk);
+            TL_C[lid] = r >> 6;
             L.s_end = min(L.s + WKA(t.chunk), WKA(t.spp));
             L.sx = L.sy = L.sz = 0.0;
             TL_HI[lid] = L.s_end;
@@ -619,9 +620,6 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           helping = true;
           TL_OWN[lid] = e & 63u;
           L.s = e >> 6;
-          const uint32_t pl = TL_PXLY[e & 63u];
-          L.px = pl & 0xFFFFu;
-          L.ly = pl >> 16;
           L.sx = L.sy = L.sz = 0.0;
         }
         wave_lds_sync();
@@ -630,6 +628,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     // ---- new sample ----
     if (((have_unit && !waiting) || helping) && !have_ray) {
       D u, v, dk[2];
+      const uint32_t pl = TL_PXLY[helping ? TL_OWN[lid] : lid];  // the unit's pixel (this lane's or its owner's)
+      L.px = pl & 0xFFFFu;
+      L.ly = pl >> 16;
       start_sample_uv<D>(kargs<D>(), L, u, v);
       for (;;) {  // randomPointInUnitDisk, rand.zig:30-36
         dk[0] = rrange_m11<D>(L.rs);
@@ -788,7 +789,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       if (L.s != L.s_end && tail && L.s == TL_HI[lid]) waiting = true;  // the rest went to other lanes
       if (L.s == L.s_end) {
         const uint32_t npix = WKA(t.row_count) * WKA(t.W);
-        double* dst = WKA(t.partial) + ((size_t)L.c * npix + (size_t)L.ly * WKA(t.W) + L.px) * 3;
+        const uint32_t pl = TL_PXLY[lid];
+        double* dst = WKA(t.partial) + ((size_t)TL_C[lid] * npix + (size_t)(pl >> 16) * WKA(t.W) + (pl & 0xFFFFu)) * 3;
         dst[0] = L.sx;
         dst[1] = L.sy;
         dst[2] = L.sz;
@@ -814,7 +816,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         TL_READY[lid] = rdy;
         if (L.s == L.s_end) {
           const uint32_t npix = WKA(t.row_count) * WKA(t.W);
-          double* dst = WKA(t.partial) + ((size_t)L.c * npix + (size_t)L.ly * WKA(t.W) + L.px) * 3;
+          const uint32_t pl = TL_PXLY[lid];
+          double* dst = WKA(t.partial) + ((size_t)TL_C[lid] * npix + (size_t)(pl >> 16) * WKA(t.W) + (pl & 0xFFFFu)) * 3;
           dst[0] = L.sx;
           dst[1] = L.sy;
           dst[2] = L.sz;
@@ -838,6 +841,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 #undef TL_PXLY
 #undef TL_LIST
 #undef TL_OWN
+#undef TL_C
   if constexpr (MODE == 2) {
     WSTAMP(0)
     if (lid == 0)

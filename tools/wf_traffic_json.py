@@ -1,5 +1,5 @@
 """HBM traffic of one wavefront frame (wf_extend + wf_shade, every bounce
-launch of the frame, + wf_finish) from the FETCH_SIZE / WRITE_SIZE PMC passes of
+launch of the frame, + the drain wf_drain / wf_finish) from the FETCH_SIZE / WRITE_SIZE PMC passes of
 tools/gpu_pmc_wf.sh -> profiles/<tag>/wf_traffic.json, read by bench.py for
 wavefront_variant.roofline.traffic.  FETCH_SIZE is doubled (gfx950 tallies
 128-B reads at 64 B, MI355X_MICROARCH.md §HBM); units are KB (rocprofv3).
@@ -11,7 +11,7 @@ import sys
 
 fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
 frames = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4].isdigit() else 1
-KERNELS = ("wf_extend", "wf_shade", "wf_step", "wf_finish")
+KERNELS = ("wf_extend", "wf_shade", "wf_step", "wf_finish", "wf_drain")
 FUSED = "--split" not in sys.argv  # the engine form the passes ran (RTW_WF_FUSED)
 
 
@@ -38,7 +38,7 @@ res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", 
        "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one 1200x675x500 f64 "
                  "wavefront render (tools/prof_run.py wf64); bytes = 2*FETCH_SIZE + WRITE_SIZE (KB x 1024), "
-                 "summed over every bounce launch of the frame (wf_step, or wf_extend + wf_shade) and its wf_finish "
-                 "(in-register drain)"}
+                 "summed over every bounce launch of the frame (wf_step, or wf_extend + wf_shade) and its in-register "
+                 "drain (wf_drain, or wf_finish with RTW_WF_DRAIN=0)"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
