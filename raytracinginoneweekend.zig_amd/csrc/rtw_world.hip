@@ -500,6 +500,10 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 #define TL_LIST tail_rows[wv][3]
 #define TL_OWN tail_rows[wv][4]  // a helper's owner lane
 #define TL_C tail_rows[wv][5]    // the unit's chunk
+  // The lane's f64 chunk sum (a helper's: the radiance of the sample it
+  // traces) lives in LDS too: it changes only when a sample ends.
+  __shared__ double home_sum[kWorldBlock / 64][3][64];
+#define HS(k) home_sum[wv][k][lid]
   // (The unit's pixel and chunk live only in these rows, read where used —
   // sample start, chunk-sum publish — instead of VGPRs across the loop.)
   // The world's fields are re-read from the kernel argument where used
@@ -517,7 +521,6 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   const uint32_t lid = lane_id();
   Lane<D> L;
   L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
-  L.sx = L.sy = L.sz = 0.0;
   L.rs = 0;
   L.skip = -1;
   // rayColor forward (main.zig:103-122): a sample's radiance is nonzero only at
@@ -568,7 +571,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
             L.s = (r >> 6) * WKA(t.chunk);
             TL_C[lid] = r >> 6;
             L.s_end = min(L.s + WKA(t.chunk), WKA(t.spp));
-            L.sx = L.sy = L.sz = 0.0;
+            HS(0) = HS(1) = HS(2) = 0.0;
             TL_HI[lid] = L.s_end;
             TL_READY[lid] = 0u;
             TL_PXLY[lid] = px | (ly << 16);
@@ -620,7 +623,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           helping = true;
           TL_OWN[lid] = e & 63u;
           L.s = e >> 6;
-          L.sx = L.sy = L.sz = 0.0;
+          HS(0) = HS(1) = HS(2) = 0.0;
         }
         wave_lds_sync();
       }
@@ -653,9 +656,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
           const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
-          L.sx += c.x;
-          L.sy += c.y;
-          L.sz += c.z;
+          HS(0) += c.x;
+          HS(1) += c.y;
+          HS(2) += c.z;
           ended = true;
         } else {
           // Hit record of the winner (object space, then the wrappers back).
@@ -702,9 +705,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
           if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
             const V c = mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p));
-            L.sx += c.x;
-            L.sy += c.y;
-            L.sz += c.z;
+            HS(0) += c.x;
+            HS(1) += c.y;
+            HS(2) += c.z;
             ended = true;
           } else {
             V ndir, att;
@@ -775,9 +778,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     if (ended && helping) {  // a sample of another lane's unit: its radiance to that lane's ring
       const uint32_t j = L.s % kTailWin, o = TL_OWN[lid];
       double* rg = WKA(ring) + ((size_t)(blockIdx.x * kWorldBlock + wv * 64u + o) * kTailWin + j) * 3;
-      rg[0] = L.sx;
-      rg[1] = L.sy;
-      rg[2] = L.sz;
+      rg[0] = HS(0);
+      rg[1] = HS(1);
+      rg[2] = HS(2);
       atomicOr(&TL_READY[o], 1u << j);
       helping = false;
       have_ray = false;
@@ -791,9 +794,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         const uint32_t npix = WKA(t.row_count) * WKA(t.W);
         const uint32_t pl = TL_PXLY[lid];
         double* dst = WKA(t.partial) + ((size_t)TL_C[lid] * npix + (size_t)(pl >> 16) * WKA(t.W) + (pl & 0xFFFFu)) * 3;
-        dst[0] = L.sx;
-        dst[1] = L.sy;
-        dst[2] = L.sz;
+        dst[0] = HS(0);
+        dst[1] = HS(1);
+        dst[2] = HS(2);
         have_unit = false;
       }
     }
@@ -805,22 +808,24 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       if (waiting) {
         uint32_t rdy = TL_READY[lid];
         const double* rb = WKA(ring) + (size_t)(blockIdx.x * kWorldBlock + threadIdx.x) * kTailWin * 3;
+        double sx = HS(0), sy = HS(1), sz = HS(2);
         while (L.s != L.s_end && ((rdy >> (L.s % kTailWin)) & 1u)) {
           const uint32_t j = L.s % kTailWin;
-          L.sx += rb[3 * j];
-          L.sy += rb[3 * j + 1];
-          L.sz += rb[3 * j + 2];
+          sx += rb[3 * j];
+          sy += rb[3 * j + 1];
+          sz += rb[3 * j + 2];
           rdy &= ~(1u << j);
           L.s++;
         }
+        HS(0) = sx, HS(1) = sy, HS(2) = sz;
         TL_READY[lid] = rdy;
         if (L.s == L.s_end) {
           const uint32_t npix = WKA(t.row_count) * WKA(t.W);
           const uint32_t pl = TL_PXLY[lid];
           double* dst = WKA(t.partial) + ((size_t)TL_C[lid] * npix + (size_t)(pl >> 16) * WKA(t.W) + (pl & 0xFFFFu)) * 3;
-          dst[0] = L.sx;
-          dst[1] = L.sy;
-          dst[2] = L.sz;
+          dst[0] = sx;
+          dst[1] = sy;
+          dst[2] = sz;
           have_unit = false;
           waiting = false;
         }
@@ -842,6 +847,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 #undef TL_LIST
 #undef TL_OWN
 #undef TL_C
+#undef HS
   if constexpr (MODE == 2) {
     WSTAMP(0)
     if (lid == 0)
