@@ -518,7 +518,7 @@ WsLayout ws_layout(const rtw_params* p) {
   if (p->engine == RTW_ENGINE_WAVEFRONT) {
     const size_t segs = wf_segs(p), n = segs * rtwk::kSegCap;
     const size_t r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
-    w.total += 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * 24) + 2 * al256(n * 4) +
+    w.total += 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * sizeof(rtwk::HomeRec)) +
                2 * al256(segs * 4) + al256(segs * 8) + al256(n * rtwk::kDrainWin * 24);
   }
   return w;
@@ -712,9 +712,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   };
   a.hit_t = reinterpret_cast<R*>(take(n * sizeof(R)));
   a.hit_k = reinterpret_cast<int32_t*>(take(n * 4));
-  a.home_sum = reinterpret_cast<double*>(take(n * 24));
-  a.home_unit = reinterpret_cast<uint32_t*>(take(n * 4));
-  a.home_s = reinterpret_cast<uint32_t*>(take(n * 4));
+  a.home = reinterpret_cast<rtwk::HomeRec*>(take(n * sizeof(rtwk::HomeRec)));
   uint32_t* seg_a = reinterpret_cast<uint32_t*>(take(segs * 4));
   uint32_t* seg_b = reinterpret_cast<uint32_t*>(take(segs * 4));
   a.seg_resv = reinterpret_cast<uint32_t*>(take(segs * 8));

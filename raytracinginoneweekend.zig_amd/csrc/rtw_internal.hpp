@@ -151,6 +151,14 @@ constexpr size_t kCoopLdsBytes = (kTraceBlock / 64) * 768;
 // runs on the same XCD every launch (fixed grid, round-robin dispatch).
 constexpr uint32_t kSegCap = 64;  // paths per segment (one 64-lane wave round)
 constexpr uint32_t kDrainWin = 32;  // wf_drain: samples of a unit dealt ahead of its fold (ring entries per slot)
+// A home slot of the wavefront engine, one 32-B record (one memory sector):
+// a sample end reads and updates the three fields together (separate arrays
+// touched three sectors per access, partially).
+struct alignas(32) HomeRec {
+  double sum[3];      // f64 chunk sum of the unit's finished samples
+  uint32_t unit, s;   // the unit, the sample in flight
+};
+static_assert(sizeof(HomeRec) == 32, "HomeRec is one 32-B sector");
 template <typename R>
 struct PathBuf {
   R *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz, *tm;
@@ -172,9 +180,7 @@ struct WfArgs {
   PathBuf<R> in, out;
   R* hit_t;         // [queue position of `in`] root of the winner
   int32_t* hit_k;   // [queue position of `in`] table position of the winner, -1 = miss
-  double* home_sum; // [slot][3]
-  uint32_t* home_unit;
-  uint32_t* home_s;
+  HomeRec* home;    // [slot] the slot's unit, sample index and f64 chunk sum
   uint32_t* seg_in;    // [segment] live paths in `in`
   uint32_t* seg_out;   // [segment] live paths written to `out` (shade)
   uint32_t* seg_resv;  // [segment][2] unit reservoir [next, end)

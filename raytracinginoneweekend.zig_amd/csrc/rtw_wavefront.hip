@@ -231,9 +231,10 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
   bool need_unit = false, need_sample = false;
   uint32_t unit = 0, s = 0;
   if (ended) {
-    unit = A.home_unit[slot];
-    s = A.home_s[slot] + 1u;
-    double* hs = A.home_sum + 3 * (size_t)slot;
+    HomeRec& h = A.home[slot];
+    unit = h.unit;
+    s = h.s + 1u;
+    double* hs = h.sum;
     double sx = hs[0], sy = hs[1], sz = hs[2];
     if (miss) {
       const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
@@ -251,7 +252,7 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
       need_unit = true;
     } else {
       if (miss) hs[0] = sx, hs[1] = sy, hs[2] = sz;
-      A.home_s[slot] = s;
+      h.s = s;
       need_sample = true;
     }
   }
@@ -259,9 +260,10 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
     uint32_t px, ly, c;
     decode_unit(A.t, unit, px, ly, c);
     s = c * A.t.chunk;
-    A.home_unit[slot] = unit;
-    A.home_s[slot] = s;
-    double* hs = A.home_sum + 3 * (size_t)slot;
+    HomeRec& h = A.home[slot];
+    h.unit = unit;
+    h.s = s;
+    double* hs = h.sum;
     // A zero the optimiser cannot hoist: hoisted out of the kernel's loop, the
     // constant vector of this store was kept in scratch (24 B per lane written
     // every launch: ~20 GB per frame of the fused engine's PMC traffic).
@@ -315,9 +317,10 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
         uint32_t px, ly, c;
         decode_unit(A.t, unit, px, ly, c);
         const uint32_t s = c * A.t.chunk;
-        A.home_unit[slot] = unit;
-        A.home_s[slot] = s;
-        A.home_sum[3 * (size_t)slot] = A.home_sum[3 * (size_t)slot + 1] = A.home_sum[3 * (size_t)slot + 2] = 0.0;
+        HomeRec& h = A.home[slot];
+        h.unit = unit;
+        h.s = s;
+        h.sum[0] = h.sum[1] = h.sum[2] = 0.0;
         start_path(A.t, unit, s, L);
       }
       if constexpr (HIT) {
@@ -594,7 +597,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
       uint32_t slot;
       load_path(A.in, base + lid, L, slot);
       k = slot - base;
-      const uint32_t unit = A.home_unit[slot], s = A.home_s[slot];
+      const uint32_t unit = A.home[slot].unit, s = A.home[slot].s;
       uint32_t px, ly, c;
       decode_unit(A.t, unit, px, ly, c);
       L.s = s;
@@ -605,7 +608,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
       u.fold = s;
       u.ready = u.miss = 0u;
       u.live = 1u;
-      const double* hs = A.home_sum + 3 * (size_t)slot;
+      const double* hs = A.home[slot].sum;
       u.sum[0] = hs[0], u.sum[1] = hs[1], u.sum[2] = hs[2];
     }
     wave_lds_sync();
