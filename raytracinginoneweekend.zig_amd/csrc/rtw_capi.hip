@@ -974,6 +974,9 @@ int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* 
             "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu "
             "cluster_wave_tests %llu cluster_wave_skips %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8],
             st[11], st[12]);
+    if (st[13])  // wavefront engine, wf_drain
+      fprintf(stderr, "[rtw counts] drain wave iterations %llu, drained segments per wave iteration %.2f of 64\n",
+              st[13], (double)st[9] / (double)st[13]);
   }
   if (mode == 2) {
     const char* names[10] = {"refill",  "start_sample", "wide+pretest", "hit+kind",    "tail",

@@ -654,6 +654,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
           atomicAdd(A.t.stats + 1, (unsigned long long)nv);
           atomicAdd(A.t.stats + 9, (unsigned long long)nv);
           atomicAdd(A.t.stats + 10, (unsigned long long)ns);
+          atomicAdd(A.t.stats + 13, 1ull);  // drain wave iterations (lane utilisation, RTW_COUNTS_VERBOSE)
         }
       }
       // 3. A finished sample's radiance goes to its unit's ring entry.
