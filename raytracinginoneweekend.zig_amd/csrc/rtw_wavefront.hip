@@ -27,6 +27,10 @@
 
 #include "rtw_device.hpp"
 
+#ifndef RTW_RING_FENCE_WG
+#define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the drain's ring)
+#endif
+
 namespace rtwk {
 
 
@@ -671,10 +675,18 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
         atomicOr(&tab[k].ready, bit);
         have = false;
       }
-      // the ring entries written above are read by other lanes of this wave
+      // The ring entries written above are read by other lanes of THIS wave:
+      // a wavefront-scope release / acquire (no cache or counter wait — the
+      // lanes of one wave see each other's vector memory operations in order,
+      // AMDGPU memory model), not a workgroup-scope one, whose release would
+      // wait for every store of the wave to complete each iteration.
+#if RTW_RING_FENCE_WG
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+      wave_lds_sync();
+#endif
       // 4. Owners fold their ready samples in sample order (main.zig:393); a
       // unit done publishes its chunk sum and the slot takes the next unit.
       bool need_unit = false;

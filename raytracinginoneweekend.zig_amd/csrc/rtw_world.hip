@@ -33,6 +33,10 @@
 #define RTW_WORLD_TOPCACHE 1
 #endif
 
+#ifndef RTW_RING_FENCE_WG
+#define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the tail ring)
+#endif
+
 namespace rtwk {
 
 // MODE 2 (-DRTW_MEASURE, RTW_WORLD_PHASE=1): s_memtime stamps per phase,
@@ -802,9 +806,15 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     }
     // ---- owners waiting on other lanes' samples fold their ring in order ----
     if constexpr (tail) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the ring entries written above
+      // the ring entries written above, read by other lanes of this wave
+      // (wavefront scope: as wf_drain's ring, rtw_wavefront.hip)
+#if RTW_RING_FENCE_WG
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+      wave_lds_sync();
+#endif
       if (waiting) {
         uint32_t rdy = TL_READY[lid];
         const double* rb = WKA(ring) + (size_t)(blockIdx.x * kWorldBlock + threadIdx.x) * kTailWin * 3;
