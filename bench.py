@@ -137,29 +137,65 @@ def wf_traffic(args, W, H, rc, spp):
     return round(t["traffic_bytes_per_frame"])
 
 
+_CPU_CHILD = r"""
+import json, os, sys, tempfile, time
+sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
+import rtw_oracle as O
+W, H, spp, spp_a, depth, seed, aspect = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), \
+    int(sys.argv[6]), int(sys.argv[7]), float(sys.argv[8])
+core = min(os.sched_getaffinity(0))
+os.sched_setaffinity(0, {core})  # one core, like the single-threaded reference
+d = tempfile.mkdtemp()
+cmd = O.build_cpu_port(os.path.join(d, "port.so"))  # -O3 -march=native on THIS host
+L = O.cpu_port_lib(os.path.join(d, "port.so"))
+cam = O.cover_camera(aspect)
+sc, rng = O.cover_scene(seed)
+t0 = time.perf_counter()
+O.render_cpu_port(L, sc, cam, rng, W, H, spp, depth)
+dt = time.perf_counter() - t0
+sc, rng = O.cover_scene(seed)
+t1 = time.perf_counter()
+_, _, st = O.render_tier_a(sc, cam, rng, W, H, spp_a, depth)
+dta = time.perf_counter() - t1
+print(json.dumps({"core": core, "cmd": cmd, "port_s": dt, "port_samples": W * H * spp, "tier_a_s": dta,
+                  "tier_a_samples": st["samples"]}))
+"""
+
+
 def cpu_baseline(width, height, spp_sample):
-    """Oracle Tier A (the reference's render loop restated: f64, one sequential
-    DefaultPrng(42) stream, recursive rayColor) on one core, on the same frame
-    at reduced spp.  Test infrastructure used only as the timed CPU baseline."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import rtw_oracle as O
-    O.lib()
-    sc, rng = O.cover_scene(SEED)
-    cam = O.cover_camera(ASPECT)
-    t0 = time.perf_counter()
-    _, _, st = O.render_tier_a(sc, cam, rng, width, height, spp_sample, DEPTH)
-    dt = time.perf_counter() - t0
+    """The reference's CPU render loop on ONE pinned core of this host: the
+    performance port oracle/ro_cpu_port.c (Tier A's algorithm and image, bit
+    for bit: one sequential DefaultPrng(42) stream, recursive rayColor, f64;
+    tests/test_oracle_tier_a.py), compiled here with -O3 -march=native
+    -ffp-contract=off, timed on the same frame at reduced spp in a child
+    process pinned with sched_setaffinity.  Beside it: the oracle's Tier A
+    (the checker) on a smaller sample, and Tier B on 16 threads.  Test /
+    measurement infrastructure used only as the timed CPU baseline."""
+    import subprocess
+    spp_a = max(1, spp_sample // 8)
+    out = subprocess.run([sys.executable, "-c", _CPU_CHILD, REPO, str(width), str(height), str(spp_sample), str(spp_a),
+                          str(DEPTH), str(SEED), repr(ASPECT)], check=True, capture_output=True, text=True).stdout
+    c = json.loads(out.strip().splitlines()[-1])
     try:
         cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         cpu = "unknown"
-    res = {"value": round(st["samples"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-           "kind_detail": "C restatement of the reference's loop (oracle Tier A; Zig is unbuildable here), "
-                          f"timed on {spp_sample} of {SPP} spp and reported as a per-sample rate",
+    res = {"value": round(c["port_samples"] / c["port_s"] / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "kind_detail": "C performance port of the reference's loop (oracle/ro_cpu_port.c: Tier A's algorithm and "
+                          "image bit for bit, SIMD discriminants, hoisted invariants; Zig is unbuildable here), built "
+                          f"on this host as `{c['cmd']}`, pinned to core {c['core']} (sched_setaffinity), timed on "
+                          f"{spp_sample} of {SPP} spp and reported as a per-sample rate",
            "sample": f"{width}x{height}x{spp_sample} spp cover frame (1/{SPP // spp_sample} of the spp), "
-                     f"{st['samples']} samples in {dt:.1f} s; oracle Tier A, single thread; host CPU {cpu}"}
+                     f"{c['port_samples']} samples in {c['port_s']:.1f} s; single thread; host CPU {cpu}",
+           "oracle_tier_a": {"value": round(c["tier_a_samples"] / c["tier_a_s"] / 1e6, 3), "unit": "Msamples/s",
+                             "cores": 1, "build": "oracle/Makefile (-O2 -ffp-contract=off): the checker, same image",
+                             "sample": f"{width}x{height}x{spp_a} spp in {c['tier_a_s']:.1f} s, core {c['core']}"}}
     # Beside it: the GPU's own contract (Tier B, counter RNG, pixels independent)
     # on the box's CPU share (16 threads, OpenMP over rows) — context only.
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import rtw_oracle as O
+    sc, _ = O.cover_scene(SEED)
+    cam = O.cover_camera(ASPECT)
     threads = 16
     t0 = time.perf_counter()
     _, stb = O.render_tier_b(sc, cam, width, height, 2 * spp_sample, DEPTH, threads=threads)
@@ -213,7 +249,7 @@ def world_variant(R, torch, scene, steps, warmup):
     cam = b.camera()
     p = R.make_params(s.width, s.height, s.spp, DEPTH, SEED, background=b.background)
     dw = Wd.DeviceWorld(b.desc)
-    need = R.workspace_bytes(p)
+    need = dw.workspace_bytes(p)  # + the tail dealing's rings (rtw_world_workspace_bytes)
     ws = torch.empty(need + 256, dtype=torch.uint8, device="cuda:0")
     ptr = (ws.data_ptr() + 255) & ~255
     rgb = torch.empty((s.height, s.width, 3), dtype=torch.uint8, device="cuda:0")

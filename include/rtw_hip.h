@@ -282,8 +282,16 @@ int rtw_world_destroy(rtw_world world);
 /* BVH statistics: nodes, leaves, max depth, max leaf size. */
 int rtw_world_bvh_info(rtw_world world, uint32_t info_out[4]);
 
+/* Device workspace of a world render on the CURRENT device (the world's):
+ * rtw_workspace_bytes(params) + the tail dealing's per-lane sample rings
+ * (one per lane of the persistent grid).  The rings live in the caller's
+ * workspace, so renders on different streams, each with its own workspace,
+ * are independent.  0 on error. */
+size_t rtw_world_workspace_bytes(rtw_world world, const rtw_params *params);
 /* Asynchronous render of a world (params.precision must be F64, engine
- * MEGAKERNEL); workspace sized by rtw_workspace_bytes(params). */
+ * MEGAKERNEL); workspace sized by rtw_world_workspace_bytes(world, params).
+ * A workspace of only rtw_workspace_bytes(params) bytes renders without tail
+ * dealing (the same image, a few % slower on the large scenes). */
 int rtw_world_render_device(rtw_world world, const rtw_camera *cam, const rtw_params *params,
                             void *workspace, size_t workspace_bytes, uint8_t *d_rgb, float *d_mean,
                             void *stream, rtw_timer timer);

@@ -224,6 +224,38 @@ def render_tier_a(scene: Scene, cam: Camera, rng: ZigRandom, width: int, height:
     return out, sums, st.as_dict()
 
 
+# ------------------------------------------ CPU baseline port (bench) ----
+PORT_SRC = os.path.join(HERE, "ro_cpu_port.c")
+PORT_LIB = os.path.join(HERE, "librtw_cpu_port.so")  # portable x86-64-v3 build (oracle/Makefile)
+PORT_FLAGS = ["-O3", "-march=native", "-std=gnu11", "-fPIC", "-ffp-contract=off", "-fno-fast-math"]
+
+
+def build_cpu_port(out_path: str, flags=None) -> str:
+    """Compile ro_cpu_port.c on THIS host (bench.py: -O3 -march=native, so the
+    timed port is tuned for the timing CPU); returns the gcc command line."""
+    cmd = ["gcc"] + list(flags or PORT_FLAGS) + ["-shared", "-o", out_path, PORT_SRC, "-lm"]
+    subprocess.run(cmd, check=True)
+    return " ".join(cmd[:-4] + ["ro_cpu_port.c"])
+
+
+def cpu_port_lib(path: str | None = None):
+    L = C.CDLL(path or PORT_LIB)
+    L.rp_render.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3, C.c_uint32, C.c_uint32,
+                            C.c_uint32, C.c_uint32, U64x4, C.c_void_p, C.c_uint32]
+    return L
+
+
+def render_cpu_port(L, scene: Scene, cam: Camera, rng: ZigRandom, width: int, height: int, spp: int,
+                    depth: int = 50, bg=COVER_BG, rows: int | None = None) -> np.ndarray:
+    """The CPU baseline's performance port of Tier A (ro_cpu_port.c): the same
+    image as render_tier_a, bit for bit (rows: only the first `rows` image rows
+    of the loop, main.zig:385 — a prefix of the same stream)."""
+    out = np.zeros((height, width, 3), np.uint8)
+    L.rp_render(C.byref(scene), C.byref(cam), (C.c_double * 3)(*bg), width, height, spp, depth, rng.s,
+                out.ctypes.data, height if rows is None else rows)
+    return out
+
+
 # ----------------------------------------------- README image (pin) ----
 # The reference's committed README image (RayTracingInOneWeekend.png, 600x400)
 # is a render of an EARLIER revision of generateRandomScene: the scene of the

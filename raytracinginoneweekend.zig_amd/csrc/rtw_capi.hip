@@ -489,19 +489,42 @@ int validate(const rtw_params* p) {
   return RTW_OK;
 }
 
-// Wavefront queue capacity: wf_paths rounded up to whole segments (one per wave).
+// Wavefront queue sets (RTW_WF_SETS, default kWfSets): the in-flight paths
+// are split over independent sets (queues, home slots, segment counts,
+// reservoirs, drain ring), each driven on its own HIP stream, so one set's
+// launch ramps, tails and drain overlap the other sets' bounce launches.  All
+// sets take units from the one device queue: a unit belongs to one slot of
+// one set, its chunk sum keeps its sample order, the image keeps its bits.
+constexpr uint32_t kWfMaxSets = 4;
+constexpr uint32_t kWfSets = 1;
+uint32_t wf_sets() {
+  const char* e = getenv("RTW_WF_SETS");
+  const int v = (e && *e) ? atoi(e) : (int)kWfSets;
+  return (uint32_t)std::min<int>(std::max(v, 1), (int)kWfMaxSets);
+}
+// The in-register drain: wf_drain (samples dealt to the wave's free lanes,
+// default) or wf_finish (RTW_WF_DRAIN=0: a lane runs its own slot's samples).
+// Only wf_drain uses the drain ring, so only it reserves one.
+bool wf_per_sample_drain() {
+  const char* de = getenv("RTW_WF_DRAIN");
+  return !(de && *de == '0');
+}
+// Segments of one queue set: its share of wf_paths rounded up to whole
+// segments (one per wave).
 uint32_t wf_segs(const rtw_params* p) {
   const uint32_t n = p->wf_paths ? p->wf_paths : RTW_DEFAULT_WF_PATHS;
-  return (n + rtwk::kSegCap - 1) / rtwk::kSegCap;
+  const uint32_t per_set = (n + wf_sets() - 1) / wf_sets();
+  return std::max(1u, (per_set + rtwk::kSegCap - 1) / rtwk::kSegCap);
 }
 
-// Workspace: partial chunk sums | counters (unit queue head, live-path poll
-// word) | stats | wavefront region (engine 1 only, rtw_internal.hpp WfArgs):
-// two path queues, the hit arrays, the home slots, per-segment counts (x2)
-// and unit reservoirs.
+// Workspace: partial chunk sums | counters (unit queue head, one live-path
+// poll word per queue set) | stats | wavefront region (engine 1 only,
+// rtw_internal.hpp WfArgs): per queue set two path queues, the hit arrays,
+// the home slots, per-segment counts (x2), unit reservoirs and (wf_drain
+// only) the drain ring.
 struct WsLayout {
   size_t partial_off, partial_bytes, counter_off, live_off, stats_off;
-  size_t wf_off, total;
+  size_t wf_off, wf_set_bytes, total;
 };
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk, + the fused engine's hit root, winner).
@@ -511,15 +534,18 @@ WsLayout ws_layout(const rtw_params* p) {
   w.partial_off = 0;
   w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
   w.counter_off = al256(w.partial_bytes);
-  w.live_off = w.counter_off + 64;
+  w.live_off = w.counter_off + 64;  // kWfMaxSets words
   w.stats_off = w.counter_off + 256;
   w.total = w.stats_off + 256;  // stats: 32 x u64
   w.wf_off = w.total;
+  w.wf_set_bytes = 0;
   if (p->engine == RTW_ENGINE_WAVEFRONT) {
     const size_t segs = wf_segs(p), n = segs * rtwk::kSegCap;
     const size_t r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
-    w.total += 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * sizeof(rtwk::HomeRec)) +
-               2 * al256(segs * 4) + al256(segs * 8) + al256(n * rtwk::kDrainWin * 24);
+    w.wf_set_bytes = 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * sizeof(rtwk::HomeRec)) +
+                     2 * al256(segs * 4) + al256(segs * 8) +
+                     (wf_per_sample_drain() ? al256(n * rtwk::kDrainWin * 3 * r) : 0);
+    w.total += wf_sets() * w.wf_set_bytes;
   }
   return w;
 }
@@ -675,20 +701,48 @@ rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
   return q;
 }
 
-// Thread-local pinned words the host polls for the queue length.
+// Thread-local pinned words the host polls for the queue lengths (two per
+// queue set: batches are checked one behind).
 uint32_t* poll_words() {
   thread_local uint32_t* w = nullptr;
-  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * sizeof(uint32_t), hipHostMallocPortable) != hipSuccess)
+  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * kWfMaxSets * sizeof(uint32_t), hipHostMallocPortable) !=
+                hipSuccess)
     w = nullptr;
   return w;
 }
 
-// Wavefront render: generate, then batches of kWfIters (extend, shade)
-// pairs; after each batch wf_count sums the segment counts of queue A and the
-// total is copied to pinned memory.  The host stops once a batch (checked one
-// batch behind, so the GPU never idles on the poll) left the queue empty, or
-// hands the drain to wf_finish once the live count shows retiring slots.
-// Empty batches cost only the launches: every wave reads its count first.
+// Side streams of the wavefront queue sets 1.. (set 0 runs on the caller's
+// stream), created once per device and thread; non-blocking, joined to the
+// caller's stream by events on every render.
+hipStream_t wf_side_stream(int dev, uint32_t k) {
+  thread_local std::map<std::pair<int, uint32_t>, hipStream_t> streams;
+  hipStream_t& s = streams[{dev, k}];
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
+// One queue set of the wavefront engine: its region of the workspace, its
+// stream and its host-side progress.
+template <typename R>
+struct WfSet {
+  rtwk::WfArgs<R> a;
+  rtwk::PathBuf<R> qa, qb;
+  uint32_t *seg_a = nullptr, *seg_b = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  uint64_t batch = 0;
+  bool done = false;
+  bool started = false;  // its generate kernel was enqueued
+};
+
+// Wavefront render: per queue set, generate, then batches of kWfIters bounce
+// launches; after each batch wf_count sums the segment counts of the set's
+// queue A and the total is copied to pinned memory.  The host stops a set
+// once a batch (checked one batch behind, so the GPU never idles on the poll)
+// left its queue empty, or hands the set's drain to wf_drain / wf_finish once
+// its live count shows retiring slots.  Empty batches cost only the
+// launches: every wave reads its count first.  Sets run on their own streams,
+// forked from and joined back to the caller's stream.
 constexpr uint32_t kWfBatch = 64;
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
@@ -698,57 +752,83 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     HIP_TRY(hipMemsetAsync(ws + L.partial_off, 0, L.partial_bytes, stream));
     return RTW_OK;
   }
-  const uint32_t segs = wf_segs(p);
+  const uint32_t segs = wf_segs(p), nsets = wf_sets();
   const size_t n = (size_t)segs * rtwk::kSegCap;
-  rtwk::WfArgs<R> a;
-  std::memset(&a, 0, sizeof(a));
-  a.t = ta;
-  unsigned char* b = ws + L.wf_off;
-  const rtwk::PathBuf<R> qa = carve_queue<R>(b, n), qb = carve_queue<R>(b, n);
-  auto take = [&](size_t bytes) {
-    unsigned char* q = b;
-    b += al256(bytes);
-    return q;
-  };
-  a.hit_t = reinterpret_cast<R*>(take(n * sizeof(R)));
-  a.hit_k = reinterpret_cast<int32_t*>(take(n * 4));
-  a.home = reinterpret_cast<rtwk::HomeRec*>(take(n * sizeof(rtwk::HomeRec)));
-  uint32_t* seg_a = reinterpret_cast<uint32_t*>(take(segs * 4));
-  uint32_t* seg_b = reinterpret_cast<uint32_t*>(take(segs * 4));
-  a.seg_resv = reinterpret_cast<uint32_t*>(take(segs * 8));
-  a.drain_buf = reinterpret_cast<double*>(take(n * rtwk::kDrainWin * 24));
-  a.live = reinterpret_cast<uint32_t*>(ws + L.live_off);
-  a.n_slots = (uint32_t)n;
-  a.n_segs = segs;
+  const bool per_sample = wf_per_sample_drain();
   // Units per reservoir refill (RTW_WF_BATCH, default kWfBatch): the refills'
   // atomics against the work a reservoir still holds when the queue runs dry.
   const char* be = getenv("RTW_WF_BATCH");
-  a.batch = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
+  const uint32_t refill = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
   // Persistent grids: every resident wave slot of each bounce kernel (at most
   // one wave per segment); the same grids for every launch of the frame.
+  // The drains run one wave per segment (wf_drain has no segment loop).
   const uint32_t max_grid = (segs + rtwk::kTraceBlock / 64 - 1) / (rtwk::kTraceBlock / 64);
+  if ((uint64_t)max_grid * (rtwk::kTraceBlock / 64) < segs) return fail(RTW_EINVAL, "drain grid below one wave per segment");
   // RTW_WF_GRID (development knob): N > 0 = N x the resident grid, capped at one wave per segment.
   const char* gk = getenv("RTW_WF_GRID");
   const uint32_t gmul = (gk && *gk) ? (uint32_t)std::max(1, atoi(gk)) : 1u;
+  // RTW_WF_SET_GRID (development knob): each set's bounce grid = the resident grid / N.
+  const char* sg = getenv("RTW_WF_SET_GRID");
+  const uint32_t gdiv = (sg && *sg) ? (uint32_t)std::max(1, atoi(sg)) : 1u;
   auto grid_of = [&](int kernel) {
     const uint32_t per_cu = (uint32_t)wf_bpc(dev, (int)(sizeof(R) == 4), kernel, lds);
-    return std::max(1u, std::min((uint32_t)device_cus(dev) * per_cu * gmul, max_grid));
+    return std::max(1u, std::min((uint32_t)device_cus(dev) * per_cu * gmul / gdiv, max_grid));
   };
   const uint32_t grid = grid_of(2), grid_ext = grid_of(1), grid_step = grid_of(3);
   // Fused engine (default; RTW_WF_FUSED=0: separate extend and shade kernels):
   // one kernel per bounce, the closest hit computed where the ray is made.
   const char* fz = getenv("RTW_WF_FUSED");
   const bool fused = !(fz && *fz == '0');
-  // generate -> queue A
-  a.out = qa;
-  a.seg_out = seg_a;
-  hipError_t e = fused ? WfLaunch<R>::gen_hit(a, grid_step, lds, stream) : WfLaunch<R>::gen(a, grid, 0, stream);
-  if (e != hipSuccess) return fail(RTW_EHIP, "wavefront generate launch: %s", hipGetErrorString(e));
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  for (auto& x : ev)
-    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return fail(RTW_EHIP, "hipEventCreate failed");
+  WfSet<R> set[kWfMaxSets];
+  int st = RTW_OK;
+  hipEvent_t fork = nullptr;
+  if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess || hipEventRecord(fork, stream) != hipSuccess)
+    st = fail(RTW_EHIP, "wavefront fork event failed");
+  for (uint32_t k = 0; k < nsets && st == RTW_OK; ++k) {
+    WfSet<R>& S = set[k];
+    rtwk::WfArgs<R>& a = S.a;
+    std::memset(&a, 0, sizeof(a));
+    a.t = ta;
+    unsigned char* b = ws + L.wf_off + k * L.wf_set_bytes;
+    S.qa = carve_queue<R>(b, n);
+    S.qb = carve_queue<R>(b, n);
+    auto take = [&](size_t bytes) {
+      unsigned char* q = b;
+      b += al256(bytes);
+      return q;
+    };
+    a.hit_t = reinterpret_cast<R*>(take(n * sizeof(R)));
+    a.hit_k = reinterpret_cast<int32_t*>(take(n * 4));
+    a.home = reinterpret_cast<rtwk::HomeRec*>(take(n * sizeof(rtwk::HomeRec)));
+    S.seg_a = reinterpret_cast<uint32_t*>(take(segs * 4));
+    S.seg_b = reinterpret_cast<uint32_t*>(take(segs * 4));
+    a.seg_resv = reinterpret_cast<uint32_t*>(take(segs * 8));
+    a.drain_buf = per_sample ? reinterpret_cast<R*>(take(n * rtwk::kDrainWin * 3 * sizeof(R))) : nullptr;
+    a.live = reinterpret_cast<uint32_t*>(ws + L.live_off) + k;
+    a.n_slots = (uint32_t)n;
+    a.n_segs = segs;
+    a.batch = refill;
+    S.s = k == 0 ? stream : wf_side_stream(dev, k);  // (set 0: the caller's stream, NULL = the default stream)
+    if (k > 0 && !S.s) {
+      st = fail(RTW_EHIP, "wavefront side stream creation failed");
+      break;
+    }
+    for (auto& x : S.ev)
+      if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) st = fail(RTW_EHIP, "hipEventCreate failed");
+    if (st != RTW_OK) break;
+    if (k > 0 && hipStreamWaitEvent(S.s, fork, 0) != hipSuccess) {
+      st = fail(RTW_EHIP, "wavefront fork wait failed");
+      break;
+    }
+    // generate -> queue A
+    a.out = S.qa;
+    a.seg_out = S.seg_a;
+    const hipError_t e = fused ? WfLaunch<R>::gen_hit(a, grid_step, lds, S.s) : WfLaunch<R>::gen(a, grid, 0, S.s);
+    if (e != hipSuccess) st = fail(RTW_EHIP, "wavefront generate launch: %s", hipGetErrorString(e));
+    S.started = true;
+  }
   // Termination bound (never reached by a correct kernel): every iteration
   // advances every live path by one segment.
   const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / kWfIters + 4;
@@ -757,71 +837,97 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   const char* tos = getenv("RTW_WF_TIMEOUT_S");
   const double timeout_s = (tos && *tos) ? atof(tos) : 300.0;
   const auto t_start = std::chrono::steady_clock::now();
-  // Drain in registers (wf_finish) once the polled live count falls below
-  // RTW_WF_FINISH x slots (default 1: as soon as slots start to retire, i.e.
-  // the unit queue ran dry; 0 = drain through the queues to the end).
+  // Drain in registers once a set's polled live count falls below
+  // RTW_WF_FINISH x its slots (default 1: as soon as slots start to retire,
+  // i.e. the unit queue ran dry; 0 = drain through the queues to the end).
   const char* fe = getenv("RTW_WF_FINISH");
   const double fin_frac = (fe && *fe) ? atof(fe) : 1.0;
-  // Which in-register drain: wf_drain (samples dealt to the wave's free lanes,
-  // default) or wf_finish (RTW_WF_DRAIN=0: a lane runs its own slot's samples).
-  const char* de = getenv("RTW_WF_DRAIN");
-  const bool per_sample = !(de && *de == '0');
-  int st = RTW_OK;
-  for (uint64_t batch = 0;; ++batch) {
-    for (int k = 0; k < kWfIters && st == RTW_OK; ++k) {
-      const bool even = (k & 1) == 0;
-      a.in = even ? qa : qb;
-      a.out = even ? qb : qa;
-      a.seg_in = even ? seg_a : seg_b;
-      a.seg_out = even ? seg_b : seg_a;
-      if (fused) {
-        if ((e = WfLaunch<R>::step(a, grid_step, lds, stream, stats)) != hipSuccess)
-          st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
-      } else if ((e = WfLaunch<R>::ext(a, grid_ext, lds, stream)) != hipSuccess ||
-                 (e = WfLaunch<R>::shd(a, grid, lds, stream, stats)) != hipSuccess) {
-        st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
+  uint32_t left = st == RTW_OK ? nsets : 0u;
+  while (left > 0 && st == RTW_OK) {
+    // Enqueue one batch on every running set, then look at each set's
+    // previous batch (so every stream holds a batch while the host waits).
+    for (uint32_t k = 0; k < nsets && st == RTW_OK; ++k) {
+      WfSet<R>& S = set[k];
+      if (S.done) continue;
+      rtwk::WfArgs<R>& a = S.a;
+      hipError_t e = hipSuccess;
+      for (int i = 0; i < kWfIters && e == hipSuccess; ++i) {
+        const bool even = (i & 1) == 0;
+        a.in = even ? S.qa : S.qb;
+        a.out = even ? S.qb : S.qa;
+        a.seg_in = even ? S.seg_a : S.seg_b;
+        a.seg_out = even ? S.seg_b : S.seg_a;
+        if (fused)
+          e = WfLaunch<R>::step(a, grid_step, lds, S.s, stats);
+        else if ((e = WfLaunch<R>::ext(a, grid_ext, lds, S.s)) == hipSuccess)
+          e = WfLaunch<R>::shd(a, grid, lds, S.s, stats);
       }
+      if (e != hipSuccess) {
+        st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
+        break;
+      }
+      uint32_t* pw = poll + 2 * k + (S.batch & 1);
+      if (rtwk::launch_wf_count(S.seg_a, segs, a.live, S.s) != hipSuccess ||
+          hipMemcpyAsync(pw, a.live, 4, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+          hipEventRecord(S.ev[S.batch & 1], S.s) != hipSuccess)
+        st = fail(RTW_EHIP, "wavefront poll enqueue failed");
     }
-    if (st == RTW_OK && (rtwk::launch_wf_count(seg_a, segs, a.live, stream) != hipSuccess ||
-                         hipMemcpyAsync(&poll[batch & 1], a.live, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-                         hipEventRecord(ev[batch & 1], stream) != hipSuccess))
-      st = fail(RTW_EHIP, "wavefront poll enqueue failed");
-    if (st != RTW_OK) break;
-    if (batch > 0) {
-      if (hipEventSynchronize(ev[(batch - 1) & 1]) != hipSuccess) {
+    for (uint32_t k = 0; k < nsets && st == RTW_OK; ++k) {
+      WfSet<R>& S = set[k];
+      if (S.done) continue;
+      const uint64_t b = S.batch++;
+      if (b == 0) continue;
+      if (hipEventSynchronize(S.ev[(b - 1) & 1]) != hipSuccess) {
         st = fail(RTW_EHIP, "wavefront batch failed on the device");
         break;
       }
-      const uint32_t live = poll[(batch - 1) & 1];
-      if (live == 0u) break;
-      if ((double)live < fin_frac * (double)n) {  // queue A holds the paths after this batch
-        a.in = qa;
-        a.seg_in = seg_a;
-        if ((e = per_sample ? WfLaunch<R>::drain(a, max_grid, lds, stream, stats)
-                                 : WfLaunch<R>::fin(a, max_grid, lds, stream, stats)) != hipSuccess)
-          st = fail(RTW_EHIP, "wavefront finish launch: %s", hipGetErrorString(e));
-        break;
+      const uint32_t live = poll[2 * k + ((b - 1) & 1)];
+      if (live != 0u && (double)live < fin_frac * (double)n) {  // queue A holds the paths after this batch
+        rtwk::WfArgs<R>& a = S.a;
+        a.in = S.qa;
+        a.seg_in = S.seg_a;
+        const hipError_t e = per_sample ? WfLaunch<R>::drain(a, max_grid, lds, S.s, stats)
+                                        : WfLaunch<R>::fin(a, max_grid, lds, S.s, stats);
+        if (e != hipSuccess) st = fail(RTW_EHIP, "wavefront finish launch: %s", hipGetErrorString(e));
+      }
+      if (live == 0u || (double)live < fin_frac * (double)n) {
+        S.done = true;
+        --left;
+      } else if (b > max_batches ||
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s) {
+        st = fail(RTW_EHIP, "wavefront queue did not drain after %llu batches", (unsigned long long)b);
       }
     }
-    if (batch > max_batches ||
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s) {
-      st = fail(RTW_EHIP, "wavefront queue did not drain after %llu batches", (unsigned long long)batch);
-      break;
+  }
+  // Every unit must have run: the drains ran outside the batch guard above,
+  // so check each set's end state on the device, then join its stream.
+  for (uint32_t k = 0; k < nsets; ++k) {
+    WfSet<R>& S = set[k];
+    if (!S.started) continue;
+    if (st == RTW_OK) {
+      if (rtwk::launch_wf_check_drained(S.seg_a, S.a.seg_resv, segs, ta.counter, ta.total_units, S.a.live, S.s) !=
+              hipSuccess ||
+          hipMemcpyAsync(&poll[2 * k], S.a.live, 4, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+          !S.ev[0] || hipEventRecord(S.ev[0], S.s) != hipSuccess)
+        st = fail(RTW_EHIP, "wavefront drain check failed to run");
+    }
+    if (k > 0 && S.ev[1]) {  // join: the caller's stream waits for this set
+      if (hipEventRecord(S.ev[1], S.s) != hipSuccess || hipStreamWaitEvent(stream, S.ev[1], 0) != hipSuccess) {
+        (void)hipStreamSynchronize(S.s);
+        if (st == RTW_OK) st = fail(RTW_EHIP, "wavefront join failed");
+      }
     }
   }
-  // Every unit must have run: the drain (queues or wf_finish) ran outside the
-  // batch guard above, so check its end state on the device before returning.
-  if (st == RTW_OK) {
-    if (rtwk::launch_wf_check_drained(seg_a, a.seg_resv, segs, ta.counter, ta.total_units, a.live, stream) !=
-            hipSuccess ||
-        hipMemcpyAsync(&poll[0], a.live, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipEventRecord(ev[0], stream) != hipSuccess || hipEventSynchronize(ev[0]) != hipSuccess)
+  for (uint32_t k = 0; k < nsets && st == RTW_OK; ++k) {
+    if (hipEventSynchronize(set[k].ev[0]) != hipSuccess)
       st = fail(RTW_EHIP, "wavefront drain check failed to run");
-    else if (poll[0] != 0u)
-      st = fail(RTW_EHIP, "wavefront drain left %u segments/reservoirs with work undone", poll[0]);
+    else if (poll[2 * k] != 0u)
+      st = fail(RTW_EHIP, "wavefront drain of set %u left %u segments/reservoirs with work undone", k, poll[2 * k]);
   }
-  (void)hipEventDestroy(ev[0]);
-  (void)hipEventDestroy(ev[1]);
+  for (uint32_t k = 0; k < nsets; ++k)
+    for (auto& x : set[k].ev)
+      if (x) (void)hipEventDestroy(x);
+  if (fork) (void)hipEventDestroy(fork);
   return st;
 }
 
@@ -1070,6 +1176,11 @@ size_t rtw_ws_total(const rtw_params* p) { return ws_layout(p).total; }
 size_t rtw_ws_stats_off(const rtw_params* p) { return ws_layout(p).stats_off; }
 size_t rtw_ws_counter_off(const rtw_params* p) { return ws_layout(p).counter_off; }
 int rtw_device_cus(int dev) { return device_cus(dev); }
+uint32_t rtw_total_units(const rtw_params* p) {
+  const uint32_t tiles_x = (p->width + rtwk::kTileW - 1) / rtwk::kTileW;
+  const uint32_t tiles_y = (p->row_count + rtwk::kTileH - 1) / rtwk::kTileH;
+  return tiles_x * tiles_y * 64u * n_chunks(p);  // = TraceArgs::total_units (fill_args)
+}
 void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, const rtw_params* p, unsigned char* ws) {
   fill_args(a, rtwk::SceneView<double>{}, cam, p, ws, ws_layout(p));
   a.unit_order = unit_order(kWorldUnitOrder);  // the world kernel's default (fill_args)

@@ -149,6 +149,14 @@ __device__ __forceinline__ uint32_t f64_long_lz(uint64_t draw_state) {  // proba
   }
   return lz;
 }
+// Leading zeros of x as the hardware counts them (v_ffbh_u32: 0xFFFFFFFF for
+// x == 0, a defined value, unlike __builtin_clz(0)); the callers override the
+// x < 2^20 case (f64_long_lz), so only x != 0 values reach the result.
+__device__ __forceinline__ uint32_t ffbh_u32(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // High word of Random.float(f64) for the drawn word's high half `hi` and its
 // leading-zero count `lz`: in the common case (leading one in the top 12
 // bits) three VALU ops — ffbh (clz without the zero fix: the rare branch
@@ -166,7 +174,7 @@ __device__ __forceinline__ double rnd_f64(uint64_t& st) {  // Random.float(f64)
   const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
   // exponent = 1022 - clz(v); mantissa = low 52 bits.  Common case: the
   // leading one is in the top 12 bits, i.e. in `hi`.
-  uint32_t lz = (uint32_t)__builtin_clz(hi);  // (hi == 0: undefined, overridden below)
+  uint32_t lz = ffbh_u32(hi);  // (hi < 2^20, incl. 0: overridden below)
   if (__builtin_expect(hi < 0x00100000u, 0)) lz = f64_long_lz(st);
   return __hiloint2double((int)f64_hi_bits(hi, lz), (int)lo);
 }
@@ -190,7 +198,7 @@ __device__ __forceinline__ void rnd3_f64(uint64_t s, double& a, double& b, doubl
   s2 = t2;
   const uint64_t v1 = sm_mix(t1), v2 = sm_mix(t2), v3 = sm_mix(t3);
   const uint32_t h1 = (uint32_t)(v1 >> 32), h2 = (uint32_t)(v2 >> 32), h3 = (uint32_t)(v3 >> 32);
-  uint32_t z1 = (uint32_t)__builtin_clz(h1), z2 = (uint32_t)__builtin_clz(h2), z3 = (uint32_t)__builtin_clz(h3);
+  uint32_t z1 = ffbh_u32(h1), z2 = ffbh_u32(h2), z3 = ffbh_u32(h3);
   if (__builtin_expect(min(min(h1, h2), h3) < 0x00100000u, 0)) {
     if (h1 < 0x00100000u) z1 = f64_long_lz(t1);
     if (h2 < 0x00100000u) z2 = f64_long_lz(t2);

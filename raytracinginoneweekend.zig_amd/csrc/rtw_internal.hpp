@@ -185,7 +185,8 @@ struct WfArgs {
   uint32_t* seg_out;   // [segment] live paths written to `out` (shade)
   uint32_t* seg_resv;  // [segment][2] unit reservoir [next, end)
   uint32_t* live;      // wf_count: sum of seg_in (host poll word)
-  double* drain_buf;   // wf_drain: [slot][kDrainWin][3] radiance of finished samples awaiting their fold
+  R* drain_buf;        // wf_drain: [slot][kDrainWin][3] radiance of finished samples awaiting their fold (R: the
+                       // sample's radiance is an R value; widened to f64 when folded, as the other engines add it)
   uint32_t n_slots, n_segs;
   uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
 };

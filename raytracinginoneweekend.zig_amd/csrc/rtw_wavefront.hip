@@ -559,7 +559,9 @@ __global__ void __launch_bounds__(kTraceBlock) wf_finish(WfArgs<R> A) {
 // kDrainWin samples of a unit are dealt ahead of its fold (the ring's size).
 // A unit done publishes its chunk sum; its slot then takes the next unit from
 // the segment's reservoir / the device queue (retiring when there is none),
-// so the kernel is correct whenever it runs, as wf_finish.
+// so the kernel is correct whenever it runs, as wf_finish — provided the grid
+// holds one wave per segment (it has no segment loop; the host launches
+// exactly that grid and refuses a smaller one, rtw_capi.hip run_wavefront).
 struct DrainUnit {  // 64 B per slot
   uint32_t unit, next, end, fold;  // unit id, next sample to deal, sample end, next sample to fold
   uint32_t ready, miss, live, pad; // ring bits (sample % kDrainWin): radiance stored / sample missed; unit held
@@ -666,10 +668,10 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
         const uint32_t bit = 1u << (L.s % kDrainWin);
         if (miss) {
           const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
-          double* b = A.drain_buf + ((size_t)(base + k) * kDrainWin + L.s % kDrainWin) * 3;
-          b[0] = (double)col.x;
-          b[1] = (double)col.y;
-          b[2] = (double)col.z;
+          R* b = A.drain_buf + ((size_t)(base + k) * kDrainWin + L.s % kDrainWin) * 3;
+          b[0] = col.x;
+          b[1] = col.y;
+          b[2] = col.z;
           atomicOr(&tab[k].miss, bit);
         }
         atomicOr(&tab[k].ready, bit);
@@ -697,10 +699,10 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
         while ((ready >> (fold % kDrainWin)) & 1u) {
           const uint32_t j = fold % kDrainWin;
           if ((mm >> j) & 1u) {  // only a miss adds (the other engines' `sx += col`)
-            const double* b = A.drain_buf + ((size_t)(base + lid) * kDrainWin + j) * 3;
-            sx += b[0];
-            sy += b[1];
-            sz += b[2];
+            const R* b = A.drain_buf + ((size_t)(base + lid) * kDrainWin + j) * 3;
+            sx += (double)b[0];
+            sy += (double)b[1];
+            sz += (double)b[2];
           }
           ready &= ~(1u << j);
           ++fold;

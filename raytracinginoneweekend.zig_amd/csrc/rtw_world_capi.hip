@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -27,6 +28,7 @@ void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, cons
 int rtw_launch_finalize(const rtw_params* p, unsigned char* ws, uint8_t* d_rgb, float* d_mean, hipStream_t s);
 size_t rtw_ws_stats_off(const rtw_params* p);
 size_t rtw_ws_counter_off(const rtw_params* p);
+uint32_t rtw_total_units(const rtw_params* p);
 int rtw_timer_mark(rtw_timer t, hipStream_t s, bool start);
 
 namespace {
@@ -240,8 +242,6 @@ struct rtw_world_s {
   bool has_moving = false;
   uint32_t feat = 0;  // features used (rtw_world.hip kFeat*): picks the kernel instantiation
   uint32_t info[4] = {0, 0, 0, 0};
-  void* ring = nullptr;  // tail dealing's per-lane rings (WorldArgs::ring), grown to the largest grid launched
-  size_t ring_bytes = 0;
 };
 
 extern "C" {
@@ -506,7 +506,6 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
 int rtw_world_destroy(rtw_world w) {
   if (!w) return RTW_OK;
   if (w->buf) (void)hipFree(w->buf);
-  if (w->ring) (void)hipFree(w->ring);
   delete w;
   return RTW_OK;
 }
@@ -551,6 +550,47 @@ double bvh_margin(const rtw_world_s* w, const rtw_camera* cam) {
   return 1e-7 * L + 0x1p-20 * L;
 }
 
+// The launch configuration of a world render on device `dev`: kernel
+// instantiation (feature set), register budget, LDS, persistent grid, and the
+// tail dealing's ring bytes (one kTailWin-entry f64x3 ring per lane of the
+// grid, WorldArgs::ring), which live in the caller's workspace after the
+// common region (rtw_ws_total), so renders on different streams with their
+// own workspaces never share one.
+struct WorldLaunchCfg {
+  int fs, oi;
+  size_t lds;
+  uint32_t grid;
+  size_t ring_off, ring_bytes;  // ring: [ring_off, ring_off + ring_bytes) of the workspace
+};
+WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
+  WorldLaunchCfg c;
+  c.lds = rtwk::world_lds_bytes(w->view.n_perlins);
+  // Register-allocation target (RTW_WORLD_OCC development knob overrides).
+  const char* oc = getenv("RTW_WORLD_OCC");
+  const int occ = (oc && *oc) ? atoi(oc) : world_occ_default(w);
+  // Kernel instantiation for the world's features (RTW_WORLD_FEAT=all: the
+  // general kernel, development knob for A/B; every set gives the same bits).
+  const char* fe = getenv("RTW_WORLD_FEAT");
+  c.fs = rtwk::world_feature_set((fe && !std::strcmp(fe, "all")) ? 15u : w->feat);
+  c.oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
+  static std::mutex mu;
+  static int bpc_cache[16][5] = {};
+  static size_t bpc_lds[16][5] = {};
+  int bpc;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (bpc_cache[c.fs][c.oi] == 0 || bpc_lds[c.fs][c.oi] != c.lds)
+      bpc_cache[c.fs][c.oi] = rtwk::world_blocks_per_cu(c.lds, c.oi, c.fs), bpc_lds[c.fs][c.oi] = c.lds;
+    bpc = bpc_cache[c.fs][c.oi];
+  }
+  const uint32_t units = rtw_total_units(p);
+  const uint32_t want = (units + 255) / 256;
+  c.grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
+  c.ring_off = (rtw_ws_total(p) + 255) & ~(size_t)255;
+  c.ring_bytes = (size_t)c.grid * rtwk::kWorldBlock * rtwk::kTailWin * 3 * sizeof(double);
+  return c;
+}
+
 int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
                  uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode) {
   if (!w || !cam) return rtw_fail(RTW_EINVAL, "world/camera is NULL");
@@ -575,35 +615,16 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   a.w = w->view;
   a.margin = bvh_margin(w, cam);
   a.counts = reinterpret_cast<unsigned long long*>(wsb + rtw_ws_stats_off(p));
-  const size_t lds = rtwk::world_lds_bytes(w->view.n_perlins);
-  // Register-allocation target (RTW_WORLD_OCC development knob overrides).
-  const char* oc = getenv("RTW_WORLD_OCC");
-  const int occ = (oc && *oc) ? atoi(oc) : world_occ_default(w);
-  // Kernel instantiation for the world's features (RTW_WORLD_FEAT=all: the
-  // general kernel, development knob for A/B; every set gives the same bits).
-  const char* fe = getenv("RTW_WORLD_FEAT");
-  const int fs = rtwk::world_feature_set((fe && !std::strcmp(fe, "all")) ? 15u : w->feat);
-  static int bpc_cache[16][5] = {};
-  static size_t bpc_lds[16][5] = {};
-  const int oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
-  if (bpc_cache[fs][oi] == 0 || bpc_lds[fs][oi] != lds)
-    bpc_cache[fs][oi] = rtwk::world_blocks_per_cu(lds, oi, fs), bpc_lds[fs][oi] = lds;
-  const int bpc = bpc_cache[fs][oi];
-  const uint32_t want = (a.t.total_units + 255) / 256;
-  const uint32_t grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
-  // Tail dealing (default; RTW_WORLD_TAIL=0: off): the rings of the grid's lanes.
+  const WorldLaunchCfg c = world_cfg(w, p, dev);
+  // Tail dealing (default; RTW_WORLD_TAIL=0: off) needs the rings in the
+  // workspace (rtw_world_workspace_bytes); a workspace of only
+  // rtw_workspace_bytes(params) renders without it — the same image.
   const char* te = getenv("RTW_WORLD_TAIL");
-  a.tail_deal = (te && *te == '0') ? 0u : 1u;
-  const size_t ring_need = (size_t)grid * rtwk::kWorldBlock * rtwk::kTailWin * 3 * sizeof(double);
-  if (a.tail_deal && w->ring_bytes < ring_need) {
-    if (w->ring && (hipStreamSynchronize(stream) != hipSuccess || hipFree(w->ring) != hipSuccess))
-      return rtw_fail(RTW_EHIP, "tail ring release failed");
-    w->ring = nullptr;
-    w->ring_bytes = 0;
-    if (hipMalloc(&w->ring, ring_need) != hipSuccess) return rtw_fail(RTW_EHIP, "tail ring: hipMalloc(%zu) failed", ring_need);
-    w->ring_bytes = ring_need;
-  }
-  a.ring = static_cast<double*>(w->ring);
+  a.tail_deal = ((te && *te == '0') || ws_bytes < c.ring_off + c.ring_bytes) ? 0u : 1u;
+  a.ring = a.tail_deal ? reinterpret_cast<double*>(wsb + c.ring_off) : nullptr;
+  const size_t lds = c.lds;
+  const uint32_t grid = c.grid;
+  const int oi = c.oi, fs = c.fs;
   if (timer && rtw_timer_mark(timer, stream, true) != RTW_OK) return RTW_EHIP;
   hipError_t e = rtwk::launch_world(a, grid, lds, stream, mode, oi, fs);
   if (e != hipSuccess) return rtw_fail(RTW_EHIP, "world kernel launch: %s", hipGetErrorString(e));
@@ -615,6 +636,17 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
 }  // namespace
 
 extern "C" {
+
+size_t rtw_world_workspace_bytes(rtw_world w, const rtw_params* p) {
+  if (!w || rtw_validate_params(p) != RTW_OK) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev != w->device) {
+    rtw_fail(RTW_EINVAL, "rtw_world_workspace_bytes: the world's device must be current");
+    return 0;
+  }
+  const WorldLaunchCfg c = world_cfg(w, p, dev);
+  return c.ring_off + c.ring_bytes;
+}
 
 int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
                             uint8_t* d_rgb, float* d_mean, void* stream, rtw_timer timer) {
@@ -671,7 +703,7 @@ int rtw_world_render(const rtw_camera* cam, const rtw_world_desc* desc, const rt
   if (hipSetDevice(dev) != hipSuccess) return rtw_fail(RTW_EHIP, "hipSetDevice failed");
   rtw_world w = nullptr;
   int st = rtw_world_create(desc, 0, &w);
-  const size_t wsb = rtw_ws_total(p), pix = (size_t)p->row_count * p->width * 3;
+  const size_t wsb = st == RTW_OK ? rtw_world_workspace_bytes(w, p) : 0, pix = (size_t)p->row_count * p->width * 3;
   void *ws = nullptr, *d_rgb = nullptr, *d_mean = nullptr;
   if (st == RTW_OK && (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&d_rgb, pix) != hipSuccess ||
                        (mean_out && hipMalloc(&d_mean, pix * sizeof(float)) != hipSuccess)))

@@ -19,7 +19,7 @@ import zlib
 
 import numpy as np
 
-from . import Camera, Params, RtwError, Timer, _check, camera_init, lib
+from . import RTW_EINVAL, Camera, Params, RtwError, Timer, _check, camera_init, lib
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT = 0, 1, 2, 3, 4
 XF_TRANSLATE, XF_ROTATE_Y = 0, 1
@@ -84,6 +84,8 @@ def _wlib():
     L.rtw_world_create.argtypes = [P(WorldDesc), C.c_uint32, P(C.c_void_p)]
     L.rtw_world_destroy.argtypes = [C.c_void_p]
     L.rtw_world_bvh_info.argtypes = [C.c_void_p, C.c_uint32 * 4]
+    L.rtw_world_workspace_bytes.restype = C.c_size_t
+    L.rtw_world_workspace_bytes.argtypes = [C.c_void_p, P(Params)]
     L.rtw_world_render_device.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t, C.c_void_p,
                                           C.c_void_p, C.c_void_p, C.c_void_p]
     L.rtw_world_render.argtypes = [P(Camera), P(WorldDesc), P(Params), C.c_void_p, C.c_void_p]
@@ -276,6 +278,14 @@ class DeviceWorld:
         info = (C.c_uint32 * 4)()
         _check(_wlib().rtw_world_bvh_info(self.h, info))
         return {"nodes": info[0], "leaves": info[1], "max_depth": info[2], "max_leaf": info[3]}
+
+    def workspace_bytes(self, params: Params) -> int:
+        """Device workspace of a render of this world (rtw_world_workspace_bytes:
+        the common region + the tail dealing's per-lane rings)."""
+        n = _wlib().rtw_world_workspace_bytes(self.h, C.byref(params))
+        if n == 0:
+            raise RtwError(RTW_EINVAL, lib().rtw_last_error().decode())
+        return n
 
     def render_async(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int, rgb_ptr: int,
                      mean_ptr: int | None = None, stream: int | None = None, timer: Timer | None = None):

@@ -109,19 +109,29 @@ def test_workspace_bytes(rtw):
     assert n < chunks * 1200 * 675 * 3 * 8 + 4096
 
 
-def test_workspace_bytes_wavefront(rtw):
+@pytest.mark.parametrize("sets", [1, 2, 3])
+@pytest.mark.parametrize("ring", [True, False])
+def test_workspace_bytes_wavefront(rtw, monkeypatch, sets, ring):
     """Wavefront engine: + two SoA path queues (each with the fused engine's
     hit root / winner per path), the split engine's hit arrays, the home
-    slots and wf_drain's ring of 32 f64x3 sample radiances (rtw_capi.hip
-    ws_layout) per in-flight path, + per-segment words."""
+    slots and (wf_drain only: RTW_WF_DRAIN != 0) its ring of 32 R x3 sample
+    radiances (rtw_capi.hip ws_layout) per in-flight path, + per-segment
+    words; wf_paths is split over RTW_WF_SETS queue sets, so the bytes per
+    path do not grow with the sets (exact bounds: an upper bound per path,
+    ADVICE r3)."""
+    monkeypatch.setenv("RTW_WF_SETS", str(sets))
+    monkeypatch.setenv("RTW_WF_DRAIN", "1" if ring else "0")
     base = rtw.workspace_bytes(rtw.make_params(1200, 675, 500))
     for prec, r in (("f64", 8), ("f32", 4)):
-        for n in (1 << 16, 1 << 20):
+        for n in (1 << 16, 1 << 20, 3 << 18):
             p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n)
-            per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + (24 + 4 + 4) + 32 * 24  # queues carry the fused hit
-            segs = n // 64  # one 64-path queue segment: 2 counts + a unit reservoir
+            per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + 32 + (32 * 3 * r if ring else 0)
+            segs = -(-n // (64 * sets))  # per set: one 64-path queue segment = 2 counts + a unit reservoir
+            paths = segs * 64
             extra = rtw.workspace_bytes(p) - base
-            assert n * per_path + segs * 16 <= extra <= n * per_path + segs * 16 + 64 * 256
+            lo = sets * (paths * per_path + segs * 16)
+            assert lo <= extra <= lo + sets * 64 * 256, (prec, n, extra, lo)
+            assert extra <= n * (per_path + 1) + sets * (64 * per_path + 64 * 256)  # per-path upper bound
     d = rtw.make_params(64, 36, 1, engine="wavefront")
     assert rtw.workspace_bytes(d) > rtw.DEFAULT_WF_PATHS * 100
 

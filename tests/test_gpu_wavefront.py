@@ -40,6 +40,15 @@ def engine_form(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(autouse=True, params=["sets1", "sets2"])
+def queue_sets(request, monkeypatch):
+    """... and one or two queue sets (RTW_WF_SETS): the in-flight paths split
+    over independent sets on their own HIP streams, sharing the device unit
+    queue (a unit still belongs to one slot, so the bits cannot change)."""
+    monkeypatch.setenv("RTW_WF_SETS", request.param[-1])
+    return int(request.param[-1])
+
+
 @pytest.fixture(scope="module")
 def cover(rtw, oracle):
     sph, mats, _ = rtw.cover_scene(42)
@@ -135,8 +144,8 @@ def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
     assert_identical(outs[0], outs[1], f"config2 {precision}")
 
 
-@pytest.mark.parametrize("w,spp,paths", [(400, 128, 360_000), (1200, 64, 0), (160, 40, 64)])
-def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, drain):
+@pytest.mark.parametrize("w,spp,paths", [(400, 128, 360_000), (1200, 64, 0), (160, 40, 64), (160, 40, 256)])
+def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, drain, queue_sets):
     """Statistics pass: the wavefront shades exactly W*H*spp samples and the
     megakernel's number of bounce segments.  Duplicated or lost units would
     leave the image bits unchanged (a unit's samples are deterministic) but
@@ -161,6 +170,7 @@ def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, d
         assert wf["drain_segments"] < wf["segments"] and wf["drain_samples"] < wf["samples"]
         # (one 64-path segment on the sky units the queue deals last: every
         # slot's last unit ends in the same bounce, so no poll sees slots
-        # retiring and the drain may not run at all)
-        if paths != 64:
+        # retiring and the drain may not run at all; 256 paths, split over
+        # at most 2 sets, is the small case whose drain must run)
+        if (paths or rtw.DEFAULT_WF_PATHS) // queue_sets > 64:
             assert wf["drain_segments"] > 0 and wf["drain_samples"] > 0

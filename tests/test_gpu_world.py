@@ -127,7 +127,7 @@ def test_cornell_full_frame_equals_oracle(rtw, oracle, W, earth):
 def _render_dev(rtw, W, b, cam, p, linear):
     import torch
     dw = W.DeviceWorld(b.desc, linear=linear)
-    need = rtw.workspace_bytes(p)
+    need = dw.workspace_bytes(p)
     ws = torch.empty(need + 256, dtype=torch.uint8, device="cuda:0")
     ptr = (ws.data_ptr() + 255) & ~255
     rgb = torch.empty((p.row_count, p.width, 3), dtype=torch.uint8, device="cuda:0")
@@ -176,6 +176,42 @@ def test_world_register_budgets_agree(rtw, W, earth, scene, w, spp, monkeypatch)
             outs.append((rgb, mean))
     for rgb, mean in outs[1:]:
         assert (rgb == outs[0][0]).all() and np.array_equal(mean.view(np.uint32), outs[0][1].view(np.uint32))
+
+
+def test_world_rings_in_caller_workspace(rtw, W, earth):
+    """The tail dealing's per-lane rings live in the caller's workspace
+    (rtw_world_workspace_bytes; ADVICE r3: they were one allocation per world,
+    shared by every launch): two renders of ONE world issued on two streams,
+    each with its own workspace, are independent and bit-identical; a
+    workspace of only rtw_workspace_bytes(params) renders without tail
+    dealing, the same image."""
+    import torch
+    b = built(W, 6, earth)
+    cam = b.camera()
+    p = params(rtw, b, 200, 200, 32)
+    dw = W.DeviceWorld(b.desc)
+    full, base = dw.workspace_bytes(p), rtw.workspace_bytes(p)
+    assert full > base + 64 * 32 * 24  # at least one wave's rings
+    outs = []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    wss = [torch.empty(full + 256, dtype=torch.uint8, device="cuda:0") for _ in streams]
+    rgbs = [torch.empty((p.row_count, p.width, 3), dtype=torch.uint8, device="cuda:0") for _ in streams]
+    torch.cuda.synchronize()
+    for rep in range(3):  # back to back on both streams: the launches overlap
+        for s, ws, rgb in zip(streams, wss, rgbs):
+            ptr = (ws.data_ptr() + 255) & ~255
+            dw.render_async(cam, p, ptr, full, rgb.data_ptr(), None, s.cuda_stream)
+    torch.cuda.synchronize()
+    outs += [r.cpu().numpy() for r in rgbs]
+    ws = torch.empty(base + 256, dtype=torch.uint8, device="cuda:0")
+    ptr = (ws.data_ptr() + 255) & ~255
+    dw.render_async(cam, p, ptr, base, rgbs[0].data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    outs.append(rgbs[0].cpu().numpy())
+    dw.close()
+    ref = W.render_world(cam, b.desc, p)
+    for o in outs:
+        assert (o == ref).all(), diff_stats(o, ref)
 
 
 def test_small_worlds_run_linear(rtw, W, earth):

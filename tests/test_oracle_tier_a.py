@@ -84,3 +84,36 @@ def test_config0_artifact(oracle):
     ppm = b"P6\n400 225\n255\n" + img.tobytes()
     assert hashlib.sha256(ppm).hexdigest() == rec["ppm_sha256"]
     assert [round(float(x), 4) for x in img.reshape(-1, 3).mean(0)] == rec["mean_rgb"]
+
+
+@pytest.mark.parametrize("w,spp,native", [(120, 6, False), (64, 16, True)])
+def test_cpu_port_equals_tier_a(oracle, tmp_path, w, spp, native):
+    """bench.py's CPU baseline is the performance port ro_cpu_port.c (SIMD
+    two-pass closest hit, hoisted invariants, record for the winner only): its
+    image is Tier A's bit for bit, on the same stream — the prebuilt portable
+    copy and the -O3 -march=native build bench.py makes on the timing host."""
+    path = None
+    if native:
+        path = str(tmp_path / "port.so")
+        oracle.build_cpu_port(path)
+    L = oracle.cpu_port_lib(path)
+    sc, rng = oracle.cover_scene(42)
+    cam = oracle.cover_camera(16 / 9)
+    h = oracle.lib().ro_image_height(w, 16 / 9)
+    rng2 = oracle.ZigRandom(state=list(rng.s))
+    a, _, _ = oracle.render_tier_a(sc, cam, rng, w, h, spp)
+    b = oracle.render_cpu_port(L, sc, cam, rng2, w, h, spp)
+    assert (a == b).all()
+    assert list(rng.s) == list(rng2.s)  # the same number of draws
+
+
+def test_cpu_port_equals_config0_artifact(oracle):
+    """... and the committed configs[0] digest (400x225x100) through the port."""
+    import hashlib
+    import json
+
+    rec = json.load(open(os.path.join(GOLDEN, "config0_tier_a_400x225x100.json")))
+    L = oracle.cpu_port_lib()
+    sc, rng = oracle.cover_scene(42)
+    img = oracle.render_cpu_port(L, sc, oracle.cover_camera(16 / 9), rng, 400, 225, 100)
+    assert hashlib.sha256(b"P6\n400 225\n255\n" + img.tobytes()).hexdigest() == rec["ppm_sha256"]
