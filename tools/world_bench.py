@@ -26,7 +26,7 @@ def run(scene, reps=3, spp=None, width=None, linear=False):
     cam = b.camera()
     p = R.make_params(W, H, spp, 50, 42, background=b.background)
     dw = Wd.DeviceWorld(b.desc, linear=linear)
-    need = R.workspace_bytes(p)
+    need = dw.workspace_bytes(p)  # + the tail dealing's rings (rtw_world_workspace_bytes)
     ws = torch.empty(need + 256, dtype=torch.uint8, device="cuda:0")
     ptr = (ws.data_ptr() + 255) & ~255
     rgb = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
