@@ -88,23 +88,42 @@ def evidence(name):
     return os.path.join(REPO, "profiles", EVIDENCE_ROUNDS[-1], name)
 
 
-def traffic_per_launch(args, W, H, spp):
+def same_per_rank_work(c, args, W, rc, spp):
+    """Does a committed PMC evidence file (measured on ONE launch of the N=1
+    frame: c = its width, height, spp, precision) describe this rank's launch?
+    At N > 1 a rank renders rows r::N of the frame at N x spp (weak scaling),
+    i.e. the N=1 frame's samples within 1 % (the row split's remainder), with
+    the same kernel, scene and per-unit work, so the per-launch evidence
+    applies to every rank's launch; `evidence_scope` in the line says so."""
+    if (c.get("width"), c.get("precision")) != (W, args.precision) or not c.get("height") or not c.get("spp"):
+        return False
+    ev = c["height"] * c["spp"]
+    return abs(rc * spp - ev) <= 0.01 * ev
+
+
+def evidence_scope(world, W, rc, spp):
+    if world == 1:
+        return "the same launch (N=1)"
+    return (f"per-rank launch: rows r::{world} at {spp} spp = {rc * W * spp / 1e6:.1f} M samples, the N=1 frame's "
+            f"workload within 1 %; evidence measured on the N=1 launch")
+
+
+def traffic_per_launch(args, W, rc, spp):
     """HBM bytes per trace launch from the committed PMC passes of the same
-    config (evidence("traffic.json"), tools/gpu_bench_profile.sh), else None."""
+    per-rank workload (evidence("traffic.json"), tools/gpu_evidence.sh), else None."""
     path = evidence("traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None
-    c = t.get("config", {})
-    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision):
+    if not same_per_rank_work(t.get("config", {}), args, W, rc, spp):
         return None
     return round(t["traffic_bytes_per_launch"])
 
 
-def valu_issue(args, W, H, spp):
-    """VALU-issue evidence of the same config from the committed PMC passes
-    (evidence("valu_issue.json"), tools/gpu_pmc_valu.sh + tools/valu_json.py),
+def valu_issue(args, W, rc, spp):
+    """VALU-issue evidence of the same per-rank workload from the committed PMC
+    passes (evidence("valu_issue.json"), tools/gpu_pmc_valu.sh + tools/valu_json.py),
     else None: the share of SIMD cycles the VALU issues and the VALU
     instructions per wave-iteration (one bounce segment per lane)."""
     path = evidence("valu_issue.json")
@@ -112,18 +131,17 @@ def valu_issue(args, W, H, spp):
         t = json.load(open(path))
     except (OSError, ValueError):
         return None
-    c = t.get("config", {})
-    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision):
+    if not same_per_rank_work(t.get("config", {}), args, W, rc, spp):
         return None
     return {"busy_frac": t["valu_busy_frac"], "valu_per_wave_iteration": t["valu_per_wave_iteration"],
             "variant": t.get("variant"), "source": os.path.relpath(path, REPO) + " (PMC SQ_ACTIVE_INST_VALU, "
             "SQ_INSTS_VALU of one launch)"}
 
 
-def wf_traffic(args, W, H, rc, spp):
-    """HBM bytes of one wavefront frame (every wf_extend + wf_shade launch) from
-    the committed PMC passes of the same config (evidence("wf_traffic.json"),
-    tools/gpu_pmc_wf.sh), else None."""
+def wf_traffic(args, W, rc, spp):
+    """HBM bytes of one wavefront frame (every bounce launch + the drain) from
+    the committed PMC passes of the same per-rank workload and engine form
+    (evidence("wf_traffic.json"), tools/gpu_pmc_wf.sh), else None."""
     path = evidence("wf_traffic.json")
     try:
         t = json.load(open(path))
@@ -131,10 +149,16 @@ def wf_traffic(args, W, H, rc, spp):
         return None
     c = t.get("config", {})
     fused = os.environ.get("RTW_WF_FUSED", "1") != "0"
-    if (c.get("width"), c.get("height"), c.get("spp"), c.get("precision")) != (W, H, spp, args.precision) \
-            or rc != H or args.wf_paths != 0 or c.get("fused", False) != fused:
+    if not same_per_rank_work(c, args, W, rc, spp) or args.wf_paths != 0 or c.get("fused", False) != fused \
+            or c.get("sets", 1) != wf_sets():
         return None
     return round(t["traffic_bytes_per_frame"])
+
+
+def wf_sets():
+    """Queue sets of the wavefront engine (RTW_WF_SETS, else the library default)."""
+    import rtw_amd as R
+    return int(os.environ.get("RTW_WF_SETS") or R.DEFAULT_WF_SETS)
 
 
 _CPU_CHILD = r"""
@@ -338,12 +362,13 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     gbs = byts / (ms * 1e-3) / 1e9
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
-            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS,
+            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
+                         "evidence_scope": evidence_scope(world, W, rc, spp),
                          "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
-                                   + " (all bounce launches of one frame) + wf_finish",
+                                   + " (all bounce launches of one frame, every queue set) + wf_drain",
                          "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts,
                          "drain_segment_frac": round(drain, 4)},
             "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
@@ -407,10 +432,13 @@ def dry_run(args):
     per = rank_times(dist, world, step_ms, step_ms, torch.device("cpu"))
     if rank == 0:
         ok = bool((img[:, 0, 0] == torch.arange(H) % world).all())
+        # the PMC evidence the GPU line would carry for this rank's launch
+        ev = {"traffic": traffic_per_launch(args, W, rc, spp), "valu_issue": valu_issue(args, W, rc, spp),
+              "wf_traffic": wf_traffic(args, W, rc, spp), "evidence_scope": evidence_scope(world, W, rc, spp)}
         print(json.dumps({"dry_run": True, "dist": {"backend": dist.get_backend() if world > 1 else None,
                                                     "world_size": world, **per},
                           "width": W, "height": H, "spp_frame": spp, "samples_all": samples.item(),
-                          "rows_interleaved_ok": ok}), flush=True)
+                          "rows_interleaved_ok": ok, "evidence": ev}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -561,13 +589,14 @@ def main():
             "bound": "valu-fp64" if args.precision == "f64" else "valu-fp32",
             "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved_tf / peak, 4),
-            "traffic": traffic_per_launch(args, W, H, spp),
+            "traffic": traffic_per_launch(args, W, rc, spp),
             "traffic_source": os.path.relpath(evidence("traffic.json"), REPO),
             "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
             "flop_per_launch": flops, "segments_per_launch": counts["segments"],
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},
-            "valu_issue": valu_issue(args, W, H, spp),
+            "valu_issue": valu_issue(args, W, rc, spp),
+            "evidence_scope": evidence_scope(world, W, rc, spp),
             "note": "megakernel is VALU-issue bound (valu_issue.busy_frac: the fraction of SIMD cycles in "
                     "which the VALU issues; f64, f32 and integer-multiply wave64 instructions each take ~4 cycles) plus "
                     "divergence; `achieved` counts only the algorithm's sphere-test flops; MFMA n/a (no "
@@ -577,7 +606,7 @@ def main():
         byts = wavefront_bytes(rend.counts(cam, params), args.precision, rc * W * n_chunks)
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, H, rc, spp),
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                     "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
                                    + " (all bounce launches of one frame) + wf_finish",
                     "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,

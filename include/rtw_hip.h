@@ -104,6 +104,9 @@ typedef struct {
 
 #define RTW_DEFAULT_CHUNK 32u
 #define RTW_DEFAULT_WF_PATHS (1u << 20)
+/* Wavefront queue sets: wf_paths is split over this many independent queue
+ * sets, each driven on its own HIP stream (env RTW_WF_SETS overrides, 1-4). */
+#define RTW_DEFAULT_WF_SETS 1u
 #define RTW_MAX_SPHERES 4096u
 
 /* ------------------------------------------------------------ queries -- */

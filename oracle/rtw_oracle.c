@@ -473,7 +473,7 @@ static int scatter_a(CtxA *cx, const RayA *r_in, const HitA *rec, V3 *att, RayA 
 /* rayColor, main.zig:103-122 (recursive; emitted == 0 for these materials) */
 static V3 ray_color_a(CtxA *cx, const RayA *r, uint32_t depth) {
   if (depth == 0) return v3(0.0, 0.0, 0.0);
-  HitA rec;
+  HitA rec = {{0, 0, 0}, {0, 0, 0}, 0, 0, 0, 0, 0}; /* (set by world_hit when it returns 1) */
   if (!world_hit(cx, r, 0.001, INFINITY, &rec)) {
     if (cx->flags & RO_BOOK1_SKY) { /* the Book-1 sky of the reference's README image (ro_render_tier_a_ex) */
       const V3 ud = vnormalized(r->dir);
@@ -553,6 +553,44 @@ void ro_render_tier_a_ex(const ro_scene *scene, const ro_camera *cam, const doub
     }
   }
   if (stats) *stats = cx.st;
+}
+/* Tier A's per-sample arithmetic (flags as ro_render_tier_a_ex) over image
+ * loop rows j in [row0, row1), with one stream PER PIXEL: DefaultPrng seeded
+ * with SplitMix64(seed + pixel) (pixel = j * W + i) instead of the reference's
+ * single stream.  Test infrastructure for the README pin's matched-filter
+ * statistic (tests/test_readme_image.py): renders of the same pixels with and
+ * without a mutated rule then share their random numbers until the mutation
+ * first changes a path (common random numbers), so their difference is the
+ * rule's systematic effect, not render noise; row bands are independent, so
+ * callers run them on several threads.  sum_out: W*H*3 f64 sums (layout of
+ * ro_render_tier_a; only the bands' rows written). */
+void ro_render_tier_a_pixel_streams(const ro_scene *scene, const ro_camera *cam, const double bg[3], uint32_t W,
+                                    uint32_t H, uint32_t spp, uint32_t depth, uint64_t seed, double *sum_out,
+                                    uint32_t flags, uint32_t row0, uint32_t row1) {
+  CtxA cx;
+  memset(&cx, 0, sizeof(cx));
+  cx.scene = scene;
+  cx.bg = vload(bg);
+  cx.flags = flags;
+  uint64_t rng[4];
+  cx.rng = rng;
+  for (uint32_t j = row0; j < H && j < row1; ++j) {
+    for (uint32_t i = 0; i < W; ++i) {
+      uint64_t sm = seed + (uint64_t)j * W + i;
+      ro_xoshiro256_seed(rng, ro_splitmix64_next(&sm));
+      V3 pc = v3(0.0, 0.0, 0.0);
+      for (uint32_t s = 0; s < spp; ++s) {
+        const double u = ((double)i + rand01(rng)) / ((double)W - 1.0);
+        const double v = ((double)j + rand01(rng)) / ((double)H - 1.0);
+        const RayA r = get_ray_a(cam, rng, u, v, NULL, !(flags & RO_BOOK1_NO_TIME));
+        pc = vadd(pc, ray_color_a(&cx, &r, depth));
+      }
+      const size_t o = ((size_t)i + (size_t)(H - j - 1) * W) * 3;
+      sum_out[o + 0] = pc.x;
+      sum_out[o + 1] = pc.y;
+      sum_out[o + 2] = pc.z;
+    }
+  }
 }
 void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double bg[3],
                       uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,

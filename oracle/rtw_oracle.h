@@ -131,6 +131,11 @@ void ro_render_tier_a_ex(const ro_scene *scene, const ro_camera *cam, const doub
                          uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
                          uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats,
                          uint32_t flags, uint32_t rows);
+/* The README pin's renderer: Tier A arithmetic, one DefaultPrng stream per
+ * pixel (seeded from seed + pixel), rows [row0, row1); f64 sums only. */
+void ro_render_tier_a_pixel_streams(const ro_scene *scene, const ro_camera *cam, const double bg[3], uint32_t W,
+                                    uint32_t H, uint32_t spp, uint32_t depth, uint64_t seed, double *sum_out,
+                                    uint32_t flags, uint32_t row0, uint32_t row1);
 void ro_render_tier_a(const ro_scene *scene, const ro_camera *cam, const double bg[3],
                       uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
                       uint64_t rng[4], uint8_t *rgb, double *sum_out, ro_stats *stats);

@@ -105,6 +105,9 @@ def lib():
         L.ro_render_tier_a_ex.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3, C.c_uint32,
                                           C.c_uint32, C.c_uint32, C.c_uint32, U64x4, C.c_void_p, C.c_void_p,
                                           C.POINTER(Stats), C.c_uint32, C.c_uint32]
+        L.ro_render_tier_a_pixel_streams.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.c_double * 3,
+                                                     C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                                     C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.ro_tierb_samples.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.c_uint32,
                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]
         L.ro_quantize.restype = C.c_uint8
@@ -336,6 +339,26 @@ def render_tier_a_ex(scene: Scene, cam: Camera, rng: ZigRandom, width: int, heig
     lib().ro_render_tier_a_ex(C.byref(scene), C.byref(cam), (C.c_double * 3)(*bg), width, height, spp, depth,
                               rng.s, out.ctypes.data, None, C.byref(st), flags, height if rows is None else rows)
     return out, st.as_dict()
+
+
+def render_pixel_streams(scene: Scene, cam: Camera, width: int, height: int, spp: int, seed: int,
+                         flags: int = BOOK1_SKY | BOOK1_NO_TIME, depth: int = 50, bg=COVER_BG,
+                         threads: int = 8) -> np.ndarray:
+    """The README pin's renderer (ro_render_tier_a_pixel_streams): Tier A's
+    arithmetic with one DefaultPrng stream per pixel, so renders with and
+    without a mutated rule share their random numbers (common random numbers);
+    row bands on `threads` threads.  Returns the linear per-pixel mean (H, W, 3)."""
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.zeros((height, width, 3), np.float64)
+    L = lib()
+    bands = [(b * height // threads, (b + 1) * height // threads) for b in range(threads)]
+
+    def run(band):
+        L.ro_render_tier_a_pixel_streams(C.byref(scene), C.byref(cam), (C.c_double * 3)(*bg), width, height, spp,
+                                         depth, seed, out.ctypes.data, flags, band[0], band[1])
+    with ThreadPoolExecutor(threads) as ex:  # (ctypes releases the GIL)
+        list(ex.map(run, bands))
+    return out / spp
 
 
 def render_tier_b(scene: Scene, cam: Camera, width: int, height: int, spp: int, depth: int = 50,

@@ -496,7 +496,7 @@ int validate(const rtw_params* p) {
 // sets take units from the one device queue: a unit belongs to one slot of
 // one set, its chunk sum keeps its sample order, the image keeps its bits.
 constexpr uint32_t kWfMaxSets = 4;
-constexpr uint32_t kWfSets = 1;
+constexpr uint32_t kWfSets = RTW_DEFAULT_WF_SETS;
 uint32_t wf_sets() {
   const char* e = getenv("RTW_WF_SETS");
   const int v = (e && *e) ? atoi(e) : (int)kWfSets;

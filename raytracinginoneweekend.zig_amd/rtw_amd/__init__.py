@@ -29,6 +29,7 @@ LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 PRECISION = {"f64": 0, "f32": 1}
 ENGINE = {"megakernel": 0, "wavefront": 1}
 DEFAULT_WF_PATHS = 1 << 20
+DEFAULT_WF_SETS = 1  # rtw_hip.h RTW_DEFAULT_WF_SETS (env RTW_WF_SETS overrides)
 DEFAULT_CHUNK = 32
 COVER_BACKGROUND = (0.70, 0.80, 1.00)
 

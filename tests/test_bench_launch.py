@@ -42,6 +42,15 @@ def test_plain_invocation_spawns_n_ranks(n):
     # configs[1] weak scaling: the 1200x675 frame at n x 500 spp
     assert (r["width"], r["height"], r["spp_frame"]) == (1200, 675, 500 * n)
     assert r["samples_all"] == 1200 * 675 * 500 * n
+    # the full key set of the line, and no silent null evidence: every rank
+    # renders the N=1 frame's samples within 1 %, so the N=1 launch's PMC
+    # evidence applies and is named
+    assert set(r) == {"dry_run", "dist", "width", "height", "spp_frame", "samples_all", "rows_interleaved_ok",
+                      "evidence"}
+    assert set(d) == {"backend", "world_size", "rank_step_ms", "rank_trace_ms", "imbalance"}
+    ev = r["evidence"]
+    assert ev["traffic"] and ev["valu_issue"]["valu_per_wave_iteration"] > 0 and ev["wf_traffic"], ev
+    assert f"rows r::{n}" in ev["evidence_scope"]
 
 
 def test_config2_is_strong_scaling_over_the_ranks():

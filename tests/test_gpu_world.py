@@ -104,6 +104,30 @@ def test_globe_config4_workload_equals_oracle(rtw, oracle, W, earth):
     assert d2["max"] == 0, d2
 
 
+@pytest.mark.parametrize("scene,dims", [(3, (600, 400, 50)), (5, (600, 400, 400))])
+def test_perlin_scenes_at_their_settings(rtw, oracle, W, earth, scene, dims):
+    """The Perlin scenes at their own main.zig settings (scene 3 two Perlin
+    spheres 600x400x50, scene 5 simple light 600x400x400; main.zig:304-308,
+    :346), the WHOLE frame on the GPU (the Perlin worlds run their own
+    feature-set instantiation at 2 waves/SIMD) against the oracle's world
+    Tier B rendered live (16 threads; ~1-10 s)."""
+    import time
+    b = built(W, scene, earth)
+    s = b.settings
+    assert (s.width, s.height, s.spp) == dims
+    g = W.render_world(b.camera(), b.desc, params(rtw, b, s.width, s.height, s.spp))
+    o = oracle.OracleWorld(scene, 42)
+    t0 = time.time()
+    ref, st = o.render_tier_b(o.camera(), s.width, s.height, s.spp, threads=16)
+    print(f"scene {scene} {s.width}x{s.height}x{s.spp} oracle: {time.time() - t0:.1f} s, {st['samples']} samples, "
+          f"{st['segments']} segments")
+    assert st["samples"] == s.width * s.height * s.spp
+    d = diff_stats(g, ref)
+    print(f"scene {scene} full frame", d)
+    assert d["max"] == 0, d  # bit-identical
+    assert g.std() > 5
+
+
 def test_cornell_full_frame_equals_oracle(rtw, oracle, W, earth):
     """The reference's default scene (scene 6, main.zig:259-293, :352-362) at
     its own settings, 600x600x200 (72 M samples, ~6.6 segments each), the

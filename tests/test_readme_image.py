@@ -132,3 +132,56 @@ def test_mutation_controls(ref, renders):
               f"{'REJECTED' if got[name] > base + REJECT else 'not detected'}")
     for name, (_, _, pinned) in MUTATIONS.items():
         assert (got[name] > base + REJECT) == pinned, (name, got[name], base)
+
+
+# Matched-filter pin.  mean|d| above mixes a rule's
+# systematic effect with the render noise of both images.  Here the oracle
+# renders with ONE DefaultPrng stream per pixel (ro_render_tier_a_pixel_streams),
+# so a render with a mutated rule and one without share their random numbers
+# (common random numbers) and their difference D is the rule's systematic
+# effect plus the noise of the paths the rule changed.  With two independent
+# estimates Da, Db (pixel-stream seeds 1 and 4) and an independent base render
+# B2 (seed 2), the statistic
+#       S = sum(Da * (ref - B2)) / sum(Da * Db)
+# has expectation 0 when the reference image follows the oracle's rule and 1
+# when it follows the mutated one (E[Da . Db] = |D_true|^2).  Controls: an
+# independent render WITH the mutation in place of the reference gives ~1,
+# one without gives ~0 — they measure the statistic's power at this budget
+# (300x200, 2x2 block means of the reference image, 16 spp).
+MF_W, MF_H, MF_SPP = 300, 200, 16
+MF_RULES = {  # name: (flags, detectable at this budget?)
+    "lambert_unnormalised (material.zig:45)": (O.MUT_LAMBERT_NONORM, True),
+    "schlick_exponent_2 (material.zig:90)": (O.MUT_SCHLICK_EXP, True),
+    "metal_absorbs_on_scattered (material.zig:64)": (O.MUT_METAL_SCATTERED, False),
+    "dielectric_draws_without_short_circuit (material.zig:81)": (O.MUT_DIEL_ALWAYS_DRAW, False),
+}
+
+
+def _mf_render(sc, flags, seed):
+    lin = O.render_pixel_streams(sc, O.readme_camera(), MF_W, MF_H, MF_SPP, seed,
+                                 flags=O.BOOK1_SKY | O.BOOK1_NO_TIME | flags)
+    return 256.0 * np.clip(np.sqrt(lin), 0.0, 0.999)  # main.zig:395-400 before the floor
+
+
+def test_matched_filter_pin():
+    ref = np.load(os.path.join(HERE, "golden", "readme_image_300x200_sum4.npz"))["sum4"].astype(np.float64) / 4.0
+    sc, _ = O.readme_scene(42)
+    base = {sd: _mf_render(sc, 0, sd) for sd in (1, 2, 3, 4)}
+    r = ref - base[2]
+    for name, (flags, detectable) in MF_RULES.items():
+        da, db = _mf_render(sc, flags, 1) - base[1], _mf_render(sc, flags, 4) - base[4]
+        den = (da * db).sum()
+        s_ref = (da * r).sum() / den
+        s_mut = (da * (_mf_render(sc, flags, 3) - base[2])).sum() / den
+        s_base = (da * (base[3] - base[2])).sum() / den
+        eff = np.sqrt(max(den, 0.0) / da.size)  # rms systematic effect per channel (LSB)
+        print(f"{name:58s} effect {eff:6.3f} LSB rms  S(ref) {s_ref:+7.3f}  controls: mutated {s_mut:+7.3f}, "
+              f"unmutated {s_base:+7.3f}")
+        if detectable:
+            # the controls separate (power), and the reference sits at the oracle's rule
+            assert abs(s_mut - 1.0) < 0.25 and abs(s_base) < 0.25, (name, s_mut, s_base)
+            assert abs(s_ref) < 0.3, (name, s_ref)
+        else:
+            # below the detection limit: the rule moves the oracle's own image by
+            # less than ~0.3 LSB rms per channel (DESIGN.md §4 records the limit)
+            assert eff < 0.3, (name, eff)
