@@ -103,10 +103,10 @@ typedef struct {
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u
-#define RTW_DEFAULT_WF_PATHS (1u << 20)
+#define RTW_DEFAULT_WF_PATHS (3u << 18) /* 786,432 in-flight paths (with two sets) */
 /* Wavefront queue sets: wf_paths is split over this many independent queue
  * sets, each driven on its own HIP stream (env RTW_WF_SETS overrides, 1-4). */
-#define RTW_DEFAULT_WF_SETS 1u
+#define RTW_DEFAULT_WF_SETS 2u
 #define RTW_MAX_SPHERES 4096u
 
 /* ------------------------------------------------------------ queries -- */

@@ -28,8 +28,8 @@ RTW_OK, RTW_EINVAL, RTW_UNSUPPORTED, RTW_EHIP, RTW_ENOMEM, RTW_ENODEV = 0, -1, -
 LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 PRECISION = {"f64": 0, "f32": 1}
 ENGINE = {"megakernel": 0, "wavefront": 1}
-DEFAULT_WF_PATHS = 1 << 20
-DEFAULT_WF_SETS = 1  # rtw_hip.h RTW_DEFAULT_WF_SETS (env RTW_WF_SETS overrides)
+DEFAULT_WF_PATHS = 3 << 18  # rtw_hip.h RTW_DEFAULT_WF_PATHS
+DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (env RTW_WF_SETS overrides)
 DEFAULT_CHUNK = 32
 COVER_BACKGROUND = (0.70, 0.80, 1.00)
 

@@ -7,6 +7,7 @@ Usage: python tools/wf_traffic_json.py FETCH_DIR WRITE_DIR OUT [frames]"""
 import csv
 import glob
 import json
+import os
 import sys
 
 fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
@@ -32,7 +33,7 @@ wk, wper = total(write_dir, "WRITE_SIZE")
 if fk == 0 or wk == 0:
     sys.exit("no bounce-kernel counter rows")
 res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", "engine": "wavefront",
-                  "fused": FUSED},
+                  "fused": FUSED, "sets": int(os.environ.get("RTW_WF_SETS") or 2), "wf_paths": 0},
        "fetch_size_kb_per_frame": fk / frames, "write_size_kb_per_frame": wk / frames,
        "per_kernel_bytes_per_frame": {k: (2 * fper.get(k, 0.0) + wper.get(k, 0.0)) * 1024 / frames for k in KERNELS},
        "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
