@@ -124,9 +124,33 @@ __device__ __forceinline__ uint32_t dealt_unit(uint32_t raw, const A& a) {
 // W + (k + 1) * gamma and any lane can evaluate any draw (coop_reject).
 constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
 constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
+#ifndef RTW_MUL64_MAD
+#define RTW_MUL64_MAD 1  // (A/B: 0 = the C multiply; profiles/r04/mul64_mad_ab.txt)
+#endif
+// z * c mod 2^64 on 32-bit lanes as three chained v_mad_u64_u32: the low
+// product lo*c_lo, then the high word accumulated as lo32(hi*c_lo + ph) and
+// lo32(lo*c_hi + that) (the laundering keeps each mad 64-bit, which the
+// optimiser would otherwise narrow back to v_mul_lo_u32 + v_add3_u32: four
+// instructions per product).  Same bits as the C multiply.
+template <uint64_t C>
+__device__ __forceinline__ uint64_t mul64c(uint64_t z) {
+#if RTW_MUL64_MAD
+  const uint32_t lo = (uint32_t)z, hi = (uint32_t)(z >> 32);
+  const uint64_t p = (uint64_t)lo * (uint32_t)C;
+  uint64_t q = (uint64_t)hi * (uint32_t)C + (p >> 32);
+  asm("" : "+v"(q));
+  // q's high word is don't-care: only the low word of r is used, so q goes
+  // in whole as the third product's addend (no zero-extension move)
+  uint64_t r = (uint64_t)lo * (uint32_t)(C >> 32) + q;
+  asm("" : "+v"(r));
+  return (r << 32) | (uint32_t)p;
+#else
+  return z * C;
+#endif
+}
 __device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  z = mul64c<0xbf58476d1ce4e5b9ULL>(z ^ (z >> 30));
+  z = mul64c<0x94d049bb133111ebULL>(z ^ (z >> 27));
   return z ^ (z >> 31);
 }
 __device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
