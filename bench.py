@@ -75,12 +75,12 @@ def parse():
     return parse_args()
 
 
-EVIDENCE_ROUNDS = ("r03", "r02", "r01")  # newest first
+EVIDENCE_ROUNDS = ("r04", "r03", "r02", "r01")  # newest first
 
 
 def evidence(name):
     """Path of a committed PMC evidence file: the newest round's copy
-    (profiles/r03, else r02, else r01)."""
+    (profiles/r04, else r03, r02, r01)."""
     for rnd in EVIDENCE_ROUNDS:
         path = os.path.join(REPO, "profiles", rnd, name)
         if os.path.exists(path):
