@@ -258,6 +258,19 @@ def world_roofline(scene, s, kernel_ms, info):
             "source": os.path.relpath(path, REPO)}
 
 
+class ClockWindow:
+    """The average shader clock over a timed loop (box-to-box
+    spreads read beside the clock): rtw_sclk_probe on a side stream, one wave
+    spinning for ~90 % of the loop's expected wall time (est_ms), read after."""
+
+    def __init__(self, R, torch, est_ms):
+        self.side = torch.cuda.Stream()
+        self.p = R.SclkProbe(self.side.cuda_stream, max(1.0, 0.9 * est_ms))
+
+    def mhz(self):
+        return round(self.p.read(), 1)
+
+
 def world_variant(R, torch, scene, steps, warmup):
     """A general-world scene on the world kernel (csrc/rtw_world.hip) at the
     scene's own main.zig settings: scene 6 (Cornell box, the reference's
@@ -278,15 +291,20 @@ def world_variant(R, torch, scene, steps, warmup):
     ptr = (ws.data_ptr() + 255) & ~255
     rgb = torch.empty((s.height, s.width, 3), dtype=torch.uint8, device="cuda:0")
     st = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
     for _ in range(max(1, warmup)):
         dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st)
     torch.cuda.synchronize()
+    warm_ms = (time.perf_counter() - w0) / max(1, warmup) * 1e3
     timers = [R.Timer() for _ in range(steps)]
+    clk = ClockWindow(R, torch, steps * warm_ms)
     a = time.perf_counter()
     for i in range(steps):
         dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st, timers[i])
     torch.cuda.synchronize()
     e = time.perf_counter() - a
+    sclk = clk.mhz()
     ms = sum(t.elapsed_ms() for t in timers) / steps
     for t in timers:
         t.close()
@@ -296,7 +314,8 @@ def world_variant(R, torch, scene, steps, warmup):
     samples = s.width * s.height * s.spp
     roof = world_roofline(scene, s, ms, info)
     return {"value": round(samples * steps / e / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(e / steps * 1e3, 3),
-            "kernel_ms": round(ms, 3), "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
+            "kernel_ms": round(ms, 3), "sclk_mhz": sclk,
+            "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
                                                   "height": s.height, "spp": s.spp, "max_depth": DEPTH},
             "bvh": info, "segments_per_sample": round(c["segments"] / samples, 3),
             "node_visits_per_segment": round(c["node_visits"] / max(1, c["segments"]), 2),
@@ -334,12 +353,16 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     p = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
                       precision=args.precision, engine="wavefront", wf_paths=args.wf_paths)
     counts = rend.counts(cam, p)  # untimed: the queue / in-register split of the segments
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
     for _ in range(max(1, args.warmup)):
         rend.render(cam, p, out=out)
     torch.cuda.synchronize()
+    warm_ms = (time.perf_counter() - w0) / max(1, args.warmup) * 1e3
     timers = [R.Timer() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
+    clk = ClockWindow(R, torch, args.steps * warm_ms)
     a = time.perf_counter()
     for i in range(args.steps):
         rend.render(cam, p, out=out, timer=timers[i])
@@ -356,13 +379,14 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     ms = sum(t.elapsed_ms() for t in timers) / len(timers)
     for t in timers:
         t.close()
+    sclk = clk.mhz()
     chunk = min(R.DEFAULT_CHUNK, spp)
     units = rc * W * ((spp + chunk - 1) // chunk)
     byts = wavefront_bytes(counts, args.precision, units)
     gbs = byts / (ms * 1e-3) / 1e9
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
-            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(),
+            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(), "sclk_mhz": sclk,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
@@ -517,11 +541,14 @@ def main():
     # Untimed: counts pass (algorithmic flops of one trace launch) + warmup.
     counts = rend.counts(cam, R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
                                             precision=args.precision))
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
     for _ in range(args.warmup):
         rend.render(cam, params, out=out)
         if world > 1:
             tg.gather(out)
     torch.cuda.synchronize()
+    warm_ms = (time.perf_counter() - w0) / max(1, args.warmup) * 1e3
 
     # One HIP-event pair per step brackets that step's trace-kernel launch on
     # the render stream (torch's current stream), read after the region.
@@ -529,6 +556,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    clk = ClockWindow(R, torch, args.steps * warm_ms) if args.warmup > 0 else None
     t0 = time.perf_counter()
     for i in range(args.steps):
         rend.render(cam, params, out=out, timer=timers[i])
@@ -543,6 +571,7 @@ def main():
     trace_ms_avg = sum(per) / len(per)
     for t in timers:
         t.close()
+    sclk = clk.mhz() if clk is not None else None
 
     dist_info = {"backend": None, "world_size": 1, "samples_per_rank": [samples_rank], "gather_ms": None}
     per_rank_t = rank_times(dist, world, elapsed / args.steps * 1e3, trace_ms_avg, torch.device("cuda", local))
@@ -591,7 +620,7 @@ def main():
             "frac": round(achieved_tf / peak, 4),
             "traffic": traffic_per_launch(args, W, rc, spp),
             "traffic_source": os.path.relpath(evidence("traffic.json"), REPO),
-            "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3),
+            "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3), "sclk_mhz": sclk,
             "flop_per_launch": flops, "segments_per_launch": counts["segments"],
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},

@@ -153,6 +153,15 @@ int rtw_timer_create(rtw_timer *out);
 int rtw_timer_destroy(rtw_timer t);
 int rtw_timer_elapsed_ms(rtw_timer t, float *ms); /* waits for the stop event */
 
+/* Shader-clock probe (diagnostic, for the bench line): one wave on `stream`
+ * (launch it on a stream other than the render's) spins for `wall_ms` of wall
+ * time and measures the SIMD clock over that window as
+ * delta(s_memtime) / delta(s_memrealtime) x 100 MHz — the average SCLK while
+ * the renders launched meanwhile run.  _end waits for the probe and frees it. */
+typedef struct rtw_sclk_probe_s *rtw_sclk_probe;
+int rtw_sclk_probe_begin(void *stream, double wall_ms, rtw_sclk_probe *out);
+int rtw_sclk_probe_end(rtw_sclk_probe p, double *mhz);
+
 /* Asynchronous render on `stream` (hipStream_t, NULL = default stream) into
  * DEVICE buffers d_rgb (W*row_count*3 bytes) and optional d_mean
  * (W*row_count*3 floats).  workspace: >= rtw_workspace_bytes(params) bytes

@@ -106,6 +106,28 @@ struct rtw_timer_s {
   bool recorded = false;
 };
 
+struct rtw_sclk_probe_s {
+  double* d = nullptr;  // [0] = MHz (device)
+  hipStream_t s = nullptr;
+};
+
+namespace {
+// One wave: spin (s_sleep between reads) until `ticks` of the 100-MHz
+// s_memrealtime counter passed; the SIMD clock = delta(s_memtime) / delta(s_memrealtime)
+// x 100 MHz (MI355X_MICROARCH.md: in-kernel clock).  Lane 0 writes the result.
+__global__ void __launch_bounds__(64) sclk_probe_kernel(unsigned long long ticks, double* out) {
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r = r0;
+  while (r - r0 < ticks) {
+    __builtin_amdgcn_s_sleep(63);
+    r = __builtin_amdgcn_s_memrealtime();
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = (double)(t1 - t0) / (double)(r - r0) * 100.0;
+}
+}  // namespace
+
 extern "C" {
 
 int rtw_abi_version(void) { return RTW_ABI_VERSION; }
@@ -1041,6 +1063,35 @@ int rtw_timer_destroy(rtw_timer t) {
   delete t;
   return RTW_OK;
 }
+int rtw_sclk_probe_begin(void* stream, double wall_ms, rtw_sclk_probe* out) {
+  if (!out) return fail(RTW_EINVAL, "probe out is NULL");
+  *out = nullptr;
+  if (!(wall_ms > 0.0 && wall_ms < 600e3)) return fail(RTW_EINVAL, "probe window %g ms outside (0, 600 s)", wall_ms);
+  auto* p = new rtw_sclk_probe_s;
+  p->s = static_cast<hipStream_t>(stream);
+  if (hipMalloc(reinterpret_cast<void**>(&p->d), sizeof(double)) != hipSuccess) {
+    delete p;
+    return fail(RTW_ENOMEM, "probe: hipMalloc failed");
+  }
+  hipLaunchKernelGGL(sclk_probe_kernel, dim3(1), dim3(64), 0, p->s, (unsigned long long)(wall_ms * 1e5), p->d);
+  if (hipGetLastError() != hipSuccess) {
+    (void)hipFree(p->d);
+    delete p;
+    return fail(RTW_EHIP, "probe kernel launch failed");
+  }
+  *out = p;
+  return RTW_OK;
+}
+int rtw_sclk_probe_end(rtw_sclk_probe p, double* mhz) {
+  if (!p || !mhz) return fail(RTW_EINVAL, "probe/mhz is NULL");
+  int st = RTW_OK;
+  if (hipStreamSynchronize(p->s) != hipSuccess || hipMemcpy(mhz, p->d, sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+    st = fail(RTW_EHIP, "probe read failed");
+  (void)hipFree(p->d);
+  delete p;
+  return st;
+}
+
 int rtw_timer_elapsed_ms(rtw_timer t, float* ms) {
   if (!t || !ms) return fail(RTW_EINVAL, "timer/ms is NULL");
   if (!t->recorded) return fail(RTW_EINVAL, "timer was never recorded");

@@ -102,6 +102,8 @@ def lib() -> C.CDLL:
     L.rtw_timer_create.argtypes = [P(C.c_void_p)]
     L.rtw_timer_destroy.argtypes = [C.c_void_p]
     L.rtw_timer_elapsed_ms.argtypes = [C.c_void_p, P(C.c_float)]
+    L.rtw_sclk_probe_begin.argtypes = [C.c_void_p, C.c_double, P(C.c_void_p)]
+    L.rtw_sclk_probe_end.argtypes = [C.c_void_p, P(C.c_double)]
     L.rtw_render_device.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.rtw_render_counts.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
@@ -194,6 +196,21 @@ def workspace_bytes(params: Params) -> int:
     if n == 0:
         _check(RTW_EINVAL)
     return int(n)
+
+
+class SclkProbe:
+    """Average shader clock (MHz) over a wall-time window (rtw_sclk_probe_*):
+    start it on a side stream, run the renders, then read()."""
+
+    def __init__(self, stream: int, wall_ms: float):
+        self.h = C.c_void_p()
+        _check(lib().rtw_sclk_probe_begin(C.c_void_p(stream), float(wall_ms), C.byref(self.h)))
+
+    def read(self) -> float:
+        mhz = C.c_double()
+        h, self.h = self.h, C.c_void_p()
+        _check(lib().rtw_sclk_probe_end(h, C.byref(mhz)))
+        return float(mhz.value)
 
 
 class Timer:

@@ -11,7 +11,7 @@ import os
 
 from conftest import REPO
 
-ROUND = "r03"
+ROUND = "r04"
 BENCH = os.path.join(REPO, "profiles", ROUND, "bench.json")
 
 
@@ -25,7 +25,7 @@ def source_round(roof, name, key):
     without a traffic_source field: the round whose file holds the value)."""
     if "traffic_source" in roof:
         return roof["traffic_source"].split("/")[1]
-    for rnd in (ROUND, "r02", "r01"):
+    for rnd in (ROUND, "r03", "r02", "r01"):
         if os.path.exists(os.path.join(REPO, "profiles", rnd, name)) and round(load(name, rnd)[key]) == roof["traffic"]:
             return rnd
     return ROUND

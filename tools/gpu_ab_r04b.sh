@@ -1,0 +1,10 @@
+# Round-4 A/B batch: megakernel xorshift from 32-bit ops (lib_x, -DRTW_XSH32=1) and the world
+# kernel's node-visit case as one scalar word (lib_sd, -DRTW_WORLD_SCALAR_DECIDE=1), each
+# after the GPU tests of its engine; then the globe's PMC passes through lib_sd.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+ENGINE=mk LIBS="lib lib_x" TESTS="tests/test_gpu_parity.py tests/test_gpu_wavefront.py" ROUNDS=3 PMC="lib_x" \
+  bash tools/gpu_ab.sh > /dev/null &&
+ENGINE=world LIBS="lib lib_sd" TESTS="tests/test_gpu_world.py" ROUNDS=3 bash tools/gpu_ab.sh > /dev/null &&
+RTW_LIB_PATH=raytracinginoneweekend.zig_amd/lib_sd/librtw_hip.so SCENE=7 bash tools/gpu_world_pmc.sh &&
+cat gpurun_out/ab_mk.txt gpurun_out/ab_world.txt
