@@ -148,19 +148,11 @@ __device__ __forceinline__ uint64_t mul64c(uint64_t z) {
   return z * C;
 #endif
 }
-#ifndef RTW_XSH32
-#define RTW_XSH32 0  // (A/B: 1 = z ^ (z >> k) from 32-bit v_alignbit / shift / xor)
-#endif
-// z ^ (z >> k), 0 < k < 32
+// z ^ (z >> k): one v_lshrrev_b64 + two v_xor_b32 (from 32-bit v_alignbit /
+// shift / xor instead: 1.3 % slower, profiles/r04/xsh32_scalar_decide_ab.txt)
 template <int K>
 __device__ __forceinline__ uint64_t xsh(uint64_t z) {
-#if RTW_XSH32
-  const uint32_t lo = (uint32_t)z, hi = (uint32_t)(z >> 32);
-  const uint32_t nlo = lo ^ __builtin_amdgcn_alignbit(hi, lo, K), nhi = hi ^ (hi >> K);
-  return ((uint64_t)nhi << 32) | nlo;
-#else
   return z ^ (z >> K);
-#endif
 }
 __device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
   z = mul64c<0xbf58476d1ce4e5b9ULL>(xsh<30>(z));

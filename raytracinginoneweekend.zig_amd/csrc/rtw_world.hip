@@ -37,10 +37,6 @@
 #define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the tail ring)
 #endif
 
-#ifndef RTW_WORLD_SCALAR_DECIDE
-#define RTW_WORLD_SCALAR_DECIDE 0  // (A/B: 1 = the node visit's case as one scalar word)
-#endif
-
 namespace rtwk {
 
 // MODE 2 (-DRTW_MEASURE, RTW_WORLD_PHASE=1): s_memtime stamps per phase,
@@ -386,24 +382,10 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       tn[c] = n;
       hit[c] = n <= f;
     }
-#if RTW_WORLD_SCALAR_DECIDE
-    // The visit's case as one scalar word (bit 0/1: child 0/1 hit by some
-    // lane; bit 2/3: child 0/1 is a leaf): wave-uniform integer logic, so the
-    // branches test SCC instead of lane-mask booleans (s_cselect -1/0, exec ANDs).
-    const uint64_t bb0 = __ballot(hit[0]), bb1 = __ballot(hit[1]);
-    uint32_t a0, a1;  // (as SALU compares: the optimiser turns `ballot != 0` into a lane select + readfirstlane)
-    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(a0) : "s"(bb0) : "scc");
-    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 2, 0" : "=s"(a1) : "s"(bb1) : "scc");
-    const uint32_t cs = a0 | a1 | ((r0 >> 31) << 2) | ((r1 >> 31) << 3);
-    if ((cs & 5u) == 5u) leaf(r0);
-    if ((cs & 10u) == 10u) leaf(r1);
-    const bool i0 = (cs & 5u) == 1u, i1 = (cs & 10u) == 2u;
-#else
     const bool any0 = __ballot(hit[0]) != 0, any1 = __ballot(hit[1]) != 0;
     if (any0 && (r0 & kLeafBit)) leaf(r0);
     if (any1 && (r1 & kLeafBit)) leaf(r1);
     const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
-#endif
     if (i0 && i1) {
       // nearer child first by vote of the lanes that hit: lanes hitting child 0
       // only or nearer-or-equal, and child 1 only or strictly nearer (masks
