@@ -37,6 +37,10 @@
 #define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the tail ring)
 #endif
 
+#ifndef RTW_WORLD_TOUCH_NEXT
+#define RTW_WORLD_TOUCH_NEXT 1  // (A/B: 0 = off; profiles/r04/world_touch_next_ab.txt)
+#endif
+
 namespace rtwk {
 
 // MODE 2 (-DRTW_MEASURE, RTW_WORLD_PHASE=1): s_memtime stamps per phase,
@@ -368,7 +372,18 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     const RTW_CONST float* nd =
         reinterpret_cast<const RTW_CONST float*>(reinterpret_cast<const RTW_CONST char*>(cn) + (node << 6));
     static_assert(kNodeWords * 4 == 64, "node record size");
+#if RTW_WORLD_TOUCH_NEXT
+    // The first word of record node + 1 — the left child whenever that child
+    // is interior (depth-first layout, rtw_world_capi.hip Builder) — loaded
+    // with this node's record (one wait covers both): the child's visit then
+    // finds its line in the scalar cache.  (A padding record follows the last;
+    // record node + 2 as well: 3 % slower, profiles/r04/world_touch_next_ab.txt.)
+    const float touch = nd[kNodeWords];
+#endif
     const uint32_t r0 = __float_as_uint(nd[12]), r1 = __float_as_uint(nd[13]);
+#if RTW_WORLD_TOUCH_NEXT
+    asm volatile("" ::"s"(touch), "s"(r0));  // (the touch's wait is the record's wait)
+#endif
     // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3
     const f2 x0 = pfma(f2{nd[0], nd[1]}, ix, oxl), x1 = pfma(f2{nd[6], nd[7]}, ix, oxh);
     const f2 y0 = pfma(f2{nd[2], nd[3]}, iy, oyl), y1 = pfma(f2{nd[8], nd[9]}, iy, oyh);

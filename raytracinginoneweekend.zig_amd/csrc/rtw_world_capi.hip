@@ -447,7 +447,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const size_t o_mat = o_tex + al(tex.size() * 8), o_perl = o_mat + al(mat.size() * 8);
   const size_t o_img = o_perl + al(perl.size() * 8), o_pix = o_img + al(img.size() * 4);
   const size_t o_node = o_pix + al(std::max(pix_bytes, (size_t)4));
-  const size_t o_order = o_node + al(std::max(bvh.nodes.size() * 4, (size_t)4));
+  // (+ two zero padding records: the traversal may load the records after the last)
+  const size_t o_order = o_node + al(bvh.nodes.size() * 4 + 2 * (size_t)rtwk::kNodeWords * 4);
   const size_t o_cull = o_order + al((size_t)std::max(n, 1u) * 4);
   const size_t total = o_cull + al(std::max(cull.size() * 4, (size_t)4));
   std::vector<unsigned char> host(total, 0);
