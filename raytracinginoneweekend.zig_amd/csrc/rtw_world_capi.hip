@@ -209,9 +209,14 @@ class Builder {
       for (uint32_t c = e - b; c > rtwk::kMaxLeafPrims; c = (c + 1) / 2) ++need;
       m = split(b, e, depth + need + 2 < rtwk::kBvhStack);
     }
-    const uint32_t c0 = m == e ? leaf(b, e) : child(b, m, depth + 1);
-    const uint32_t c1 = m == e ? (rtwk::kLeafBit | e) : child(m, e, depth + 1);
-    const Box b0 = range_box(b, m), b1 = range_box(m, e);
+    // Child 0 is built first, so an interior child 0 is record n + 1, the line
+    // the traversal loads with node n (rtw_world.hip RTW_WORLD_TOUCH_NEXT).
+    // (The child of larger surface area first instead: equal, profiles/r04/
+    // world_touch_next_ab.txt.)
+    const uint32_t lo0 = b, hi0 = m, lo1 = m, hi1 = e;
+    const uint32_t c0 = m == e ? leaf(b, e) : child(lo0, hi0, depth + 1);
+    const uint32_t c1 = m == e ? (rtwk::kLeafBit | e) : child(lo1, hi1, depth + 1);
+    const Box b0 = range_box(lo0, hi0), b1 = range_box(lo1, hi1);
     float* nd = out_.nodes.data() + (size_t)rtwk::kNodeWords * n;
     auto down = [](double x) {  // largest float <= x
       float f = (float)x;
