@@ -503,6 +503,9 @@ __device__ __forceinline__ void coop_reject_mixed(uint32_t dim, uint64_t& st, R 
   }
   uint64_t P = __ballot(pending);
   uint32_t nextq = 0;  // candidates are counted from B = st
+  // (Round 0 with each pending lane's second candidate as well, before any
+  // dealing round: 1,483 VALU per wave-iteration, 0.5 % slower;
+  // profiles/r04/coop_round0_ab.txt.)
   while (P) {
     const uint32_t m = (uint32_t)__popcll(P);  // wave-uniform (scalar)
     // c = 2^lc = 2^floor(log2(64/m)) = 2^(6 - ceil(log2 m)) (c*m <= 64): one
