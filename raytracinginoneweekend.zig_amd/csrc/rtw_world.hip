@@ -227,10 +227,11 @@ struct WHit {
   int pos;     // stored position of the winner (-1: miss)
   int orig;    // its list index
   D t;
-  bool nan;
+  uint32_t nan;  // a NaN root was seen (a u32, not a bool: it stays in a VGPR instead of a lane-mask phi
+                 // the traversal loop would copy through exec on every node visit)
 };
 __device__ __forceinline__ void accept(WHit& h, D t, int pos, int orig, D tmin) {
-  if (t != t) h.nan = true;
+  h.nan |= (uint32_t)(t != t);
   if (!(t < tmin) & ((t < h.t) | ((t == h.t) & (orig > h.orig)))) {
     h.t = t;
     h.pos = pos;
@@ -264,7 +265,7 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   h.pos = -1;
   h.orig = -1;
   h.t = (D)__builtin_huge_val();
-  h.nan = false;
+  h.nan = 0u;
   if (W.n_nodes == 0) {  // linear: wave-uniform loop, scalar-loaded records, one-ahead prefetch
     const RTW_CONST D* pr = cptr(W.prim);
     PrimRec cur = load_rec(pr);  // (a padding record follows the last primitive)
@@ -397,7 +398,10 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       tn[c] = n;
       hit[c] = n <= f;
     }
-    const bool any0 = __ballot(hit[0]) != 0, any1 = __ballot(hit[1]) != 0;
+    // (the ballots are reused by the vote below: ballots of hit[] made again
+    // there would first rebuild hit[] in VGPRs from these lane masks)
+    const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
+    const bool any0 = b0 != 0, any1 = b1 != 0;
     if (any0 && (r0 & kLeafBit)) leaf(r0);
     if (any1 && (r1 & kLeafBit)) leaf(r1);
     const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
@@ -407,7 +411,6 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       // combined in scalar ops, 32-bit popcounts).  (Ordering by the wave's
       // majority ray sign along the split axis instead visits 101 nodes per
       // segment against 84: 13 % slower, profiles/r03/world_signorder_ab.txt.)
-      const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
       const uint64_t le = wballot(tn[0] <= tn[1]), gt = wballot(tn[1] < tn[0]);
       const uint32_t v0 = popc64(b0 & (~b1 | le)), v1 = popc64(b1 & (~b0 | gt));
       const bool first0 = v0 >= v1;
@@ -672,7 +675,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         WHit h;
         WSTAMP(1)  // sample start (+ take units, loop control)
         closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
-        if (__builtin_expect(h.nan, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
+        if (__builtin_expect(h.nan != 0u, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
           const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
           HS(0) += c.x;
