@@ -37,6 +37,10 @@
 #define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the tail ring)
 #endif
 
+#ifndef RTW_WORLD_DECIDE_REFS
+#define RTW_WORLD_DECIDE_REFS 1  // the node visit's decisions as refs made before its leaf tests
+                                 // (0: as bools; profiles/r04/world_decide_refs_ab.txt)
+#endif
 #ifndef RTW_WORLD_TOUCH_NEXT
 #define RTW_WORLD_TOUCH_NEXT 1  // (A/B: 0 = off; profiles/r04/world_touch_next_ab.txt)
 #endif
@@ -401,6 +405,57 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     // (the ballots are reused by the vote below: ballots of hit[] made again
     // there would first rebuild hit[] in VGPRs from these lane masks)
     const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
+#if RTW_WORLD_DECIDE_REFS
+    // The visit's decisions as 32-bit refs (kNoRef: none) made before the leaf
+    // tests (which do not change them), by scalar compares and selects in asm:
+    // as C++ bools, LLVM kept them across the leaf calls as 64-bit lane masks
+    // (s_cselect -1 / 0, re-combined through exec at the joins), and as
+    // integers made from bools it went through VGPRs (v_cndmask +
+    // v_readfirstlane).  Globe SALU per wave-iteration 3,848 -> 3,151, -2.4 %
+    // time (profiles/r04/world_decide_refs_ab.txt).
+    constexpr uint32_t kNoRef = 0xFFFFFFFFu;  // (never a ref: interior refs < kLeafBit, leaf counts <= 2)
+    // per child c: t = (some lane hit c) ? r_c : kNoRef; then by the leaf bit of r_c,
+    // leaf ref l_c = leaf ? t : kNoRef and interior ref i_c = leaf ? kNoRef : t
+    uint32_t la, lb, ia, ib;
+    asm("s_cmp_lg_u64 %4, 0\n\ts_cselect_b32 %0, %6, -1\n\ts_bitcmp1_b32 %6, 31\n\t"
+        "s_cselect_b32 %2, -1, %0\n\ts_cselect_b32 %0, %0, -1\n\t"
+        "s_cmp_lg_u64 %5, 0\n\ts_cselect_b32 %1, %7, -1\n\ts_bitcmp1_b32 %7, 31\n\t"
+        "s_cselect_b32 %3, -1, %1\n\ts_cselect_b32 %1, %1, -1"
+        : "=&s"(la), "=&s"(lb), "=&s"(ia), "=&s"(ib)
+        : "s"(b0), "s"(b1), "s"(r0), "s"(r1)
+        : "scc");
+    uint32_t nx = ia & ib, ps = kNoRef;  // at most one interior child hit: its ref (or kNoRef)
+    if ((ia | ib) < kLeafBit) {          // both: the nearer first, by the vote of the #else branch
+      const uint64_t le = wballot(tn[0] <= tn[1]), gt = wballot(tn[1] < tn[0]);
+      const uint32_t v0 = popc64(b0 & (~b1 | le)), v1 = popc64(b1 & (~b0 | gt));
+      nx = v0 >= v1 ? r0 : r1;
+      ps = v0 >= v1 ? r1 : r0;
+    }
+    if (la != kNoRef) leaf(la);
+    if (lb != kNoRef) leaf(lb);
+    if (ps != kNoRef) {
+#if RTW_WORLD_TOPCACHE
+      stack[sp++] = top;  // (entry 0 is a dummy when the stack was empty)
+      top = ps;
+#else
+      stack[sp++] = ps;
+#endif
+    }
+    if (nx != kNoRef) {
+      node = nx;
+    } else {
+      if (sp == 0) {
+        WSTAMP(2)
+        break;
+      }
+#if RTW_WORLD_TOPCACHE
+      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)top);
+      top = stack[--sp];
+#else
+      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);
+#endif
+    }
+#else
     const bool any0 = b0 != 0, any1 = b1 != 0;
     if (any0 && (r0 & kLeafBit)) leaf(r0);
     if (any1 && (r1 & kLeafBit)) leaf(r1);
@@ -439,6 +494,7 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);  // uniform: scalar loads
 #endif
     }
+#endif
   }
 }
 
