@@ -398,7 +398,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
           const float rf = (float)r[6];
           q[12] = -(rf * rf);
         }
-        ref |= rtwk::kCullBit;
+        ref |= rtwk::kCullBit;  // (cnt <= 2 here, so no ref is all ones: the traversal's kNoRef, rtw_world.hip)
         std::memcpy(nw, &ref, 4);
       }
     }
