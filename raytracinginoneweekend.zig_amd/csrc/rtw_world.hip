@@ -41,6 +41,10 @@
 #define RTW_WORLD_DECIDE_REFS 1  // the node visit's decisions as refs made before its leaf tests
                                  // (0: as bools; profiles/r04/world_decide_refs_ab.txt)
 #endif
+#ifndef RTW_WORLD_LANE_FLAGS
+#define RTW_WORLD_LANE_FLAGS 1  // the lane's state flags as bits of one word
+                                // (0: bools; profiles/r04/world_lane_flags_ab.txt)
+#endif
 #ifndef RTW_WORLD_TOUCH_NEXT
 #define RTW_WORLD_TOUCH_NEXT 1  // (A/B: 0 = off; profiles/r04/world_touch_next_ab.txt)
 #endif
@@ -559,6 +563,17 @@ __device__ __forceinline__ V tex_value(const WV& W, uint32_t ti, D u, D v, V p) 
   }
 }
 
+// One bit of a per-lane flag word, used like a bool (RTW_WORLD_LANE_FLAGS).
+template <uint32_t BIT>
+struct LaneFlag {
+  uint32_t& w;
+  __device__ __forceinline__ operator bool() const { return (w & BIT) != 0u; }
+  __device__ __forceinline__ LaneFlag& operator=(bool v) {
+    w = v ? (w | BIT) : (w & ~BIT);
+    return *this;
+  }
+};
+
 // OCC: minimum resident workgroups per CU asked of the register allocator
 // (1 = unconstrained; chosen by A/B on MI355X, rtw_world_capi.hip).
 template <int MODE, int OCC, int FEAT>
@@ -605,9 +620,22 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // the event that ends it (a miss adds T * background, a light T * emitted),
   // so that one term joins the chunk sum directly: sx + (0 + x) == sx + x
   // (x >= +0), the oracle's `rad` (rtw_world.c sample_b) without its registers.
+#if RTW_WORLD_LANE_FLAGS
+  // The lane's state flags as bits of ONE word (a VGPR): as bools, each was a
+  // 64-bit lane mask in SGPRs for the whole loop, and at the traversal's SGPR
+  // peak the compiler spilled SGPRs to VGPR lanes (v_writelane / v_readlane,
+  // VALU instructions) around it.
+  uint32_t lane_flags = 0u;
+  LaneFlag<1u> have_unit{lane_flags};
+  LaneFlag<2u> have_ray{lane_flags};
+  LaneFlag<4u> done{lane_flags};
+  LaneFlag<8u> waiting{lane_flags};   // owner: its own samples done, waiting for the ones other lanes trace
+  LaneFlag<16u> helping{lane_flags};  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
+#else
   bool have_unit = false, have_ray = false, done = false;
   bool waiting = false;  // owner: its own samples done, waiting for the ones other lanes trace
   bool helping = false;  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
+#endif
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
   KStats st;  // MODE 2: phase stamps
