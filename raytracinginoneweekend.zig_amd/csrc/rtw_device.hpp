@@ -399,6 +399,20 @@ __device__ __forceinline__ bool in_unit_ball(const R (&x)[D]) {
     return !(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] >= (R)1);  // rand.zig:26; sqrt(t) >= 1 <=> t >= 1
 }
 
+// One bit of a per-lane flag word, used like a bool: a lane's state flags kept
+// as bits of one u32 (a VGPR) instead of bools, which the compiler holds as
+// 64-bit lane masks in SGPRs for a whole loop (rtw_world.hip
+// RTW_WORLD_LANE_FLAGS, rtw_trace.hip RTW_TRACE_LANE_FLAGS).
+template <uint32_t BIT>
+struct LaneFlag {
+  uint32_t& w;
+  __device__ __forceinline__ operator bool() const { return (w & BIT) != 0u; }
+  __device__ __forceinline__ LaneFlag& operator=(bool v) {
+    w = v ? (w | BIT) : (w & ~BIT);
+    return *this;
+  }
+};
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

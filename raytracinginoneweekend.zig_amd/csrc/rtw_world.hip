@@ -563,17 +563,6 @@ __device__ __forceinline__ V tex_value(const WV& W, uint32_t ti, D u, D v, V p) 
   }
 }
 
-// One bit of a per-lane flag word, used like a bool (RTW_WORLD_LANE_FLAGS).
-template <uint32_t BIT>
-struct LaneFlag {
-  uint32_t& w;
-  __device__ __forceinline__ operator bool() const { return (w & BIT) != 0u; }
-  __device__ __forceinline__ LaneFlag& operator=(bool v) {
-    w = v ? (w | BIT) : (w & ~BIT);
-    return *this;
-  }
-};
-
 // OCC: minimum resident workgroups per CU asked of the register allocator
 // (1 = unconstrained; chosen by A/B on MI355X, rtw_world_capi.hip).
 template <int MODE, int OCC, int FEAT>
