@@ -451,9 +451,25 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
 #ifndef RTW_WF_STEP_OCC
 #define RTW_WF_STEP_OCC 5  // profiles/r02/wf_step_ab.txt: 5 waves (32-B spill) ~3 % faster than 4
 #endif
+#ifndef RTW_WF_KARG
+// wf_step / wf_drain read their arguments through the kernarg pointer where
+// used: held in SGPRs for the whole kernel (30 queue pointers among them) they
+// were spilled to VGPR lanes around the closest hit (wf_step 93 -> 34,
+// wf_drain 291 -> 93 v_readlane / v_writelane); -0.6 to -0.9 % per wavefront
+// frame (profiles/r04/wf_karg_ab.txt).  0: the by-value argument.
+#define RTW_WF_KARG 1
+#endif
+// The kernel's argument (WfArgs, at offset 0 of the kernarg segment) through
+// a pointer the compiler cannot see through (rtw_device.hpp opaque): its
+// fields are scalar-loaded where used instead of held in SGPRs.
+template <typename R>
+__device__ __forceinline__ const WfArgs<R>& wkargs() {
+  return *(const WfArgs<R>*)opaque((const RTW_CONST WfArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr());
+}
 template <typename R, bool F32, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R> A) {
+__global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R> A_arg) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
+  const WfArgs<R>& A = RTW_WF_KARG ? wkargs<R>() : A_arg;
   const uint32_t lid = lane_id();
   if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
     if (lid == 0)
@@ -571,8 +587,9 @@ struct DrainUnit {  // 64 B per slot
 static_assert(sizeof(DrainUnit) == 64, "DrainUnit layout");
 
 template <typename R, bool F32, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A) {
+__global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A_arg) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
+  const WfArgs<R>& A = RTW_WF_KARG ? wkargs<R>() : A_arg;
   __shared__ DrainUnit tab_all[kTraceBlock / 64][kSegCap];
   __shared__ uint32_t list_all[kTraceBlock / 64][64];
   const uint32_t lid = lane_id();
