@@ -526,12 +526,17 @@ int rtw_world_bvh_info(rtw_world w, uint32_t info_out[4]) {
 
 namespace {
 
-// Default register-allocation target (waves per SIMD) from the A/B on MI355X
-// (DESIGN.md §6.3): 4 waves hide the BVH's dependent node loads and the
-// Cornell box's emission/rect mix (despite a small spill); Perlin-textured
-// worlds keep the 2-wave budget because their noise loops spill badly.
+// Default register-allocation target (waves per SIMD) from the A/Bs on MI355X
+// (DESIGN.md §6.3): 4 waves hide the BVH's dependent node loads; worlds with
+// rects or transforms (the Cornell box) run 2 % faster at the 3-wave budget
+// since round 4's register work (profiles/r04/world_occ_ab.txt; round 1: 4 was
+// best); Perlin-textured worlds keep the 2-wave budget because their noise
+// loops spill badly.
 static_assert(rtwk::kMaxXfOps == RTW_MAX_XFORM_OPS, "transform chain length");
-int world_occ_default(const rtw_world_s* w) { return w->view.n_perlins ? 1 : 4; }
+int world_occ_default(const rtw_world_s* w) {
+  if (w->view.n_perlins) return 1;
+  return (w->feat & (4u | 8u)) ? 3 : 4;  // rtw_world.hip kFeatXform | kFeatRect
+}
 
 // Widening of every BVH box test.  A computed sphere root deviates from the
 // exact intersection by at most ~sqrt(u * (hb^2 + |a c|)) / a (u = 2^-53; the
