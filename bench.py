@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="megakernel", choices=["megakernel", "wavefront"],
                     help="headline engine (the other one is reported as a variant)")
     ap.add_argument("--wf-paths", type=int, default=0, help="wavefront in-flight paths (0 = library default)")
+    ap.add_argument("--wf-sets", type=int, default=0, help="wavefront queue sets, params.wf_sets (0 = library default)")
+    ap.add_argument("--wf-drain", default="samples", choices=["samples", "slots", "none"], help="params.wf_drain")
+    ap.add_argument("--wf-form", default="fused", choices=["fused", "split"], help="params.wf_form")
     ap.add_argument("--no-wavefront-variant", action="store_true")
     ap.add_argument("--no-world-variants", action="store_true", help="skip the configs[4] globe and Cornell lines")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2],
@@ -102,10 +105,14 @@ def same_per_rank_work(c, args, W, rc, spp):
 
 
 def evidence_scope(world, W, rc, spp):
+    """What the PMC figures of a roofline (traffic, valu_issue) describe: the
+    committed passes named by its *_source fields, made in another process
+    (usually on another box) on the same workload — not this line's launch."""
     if world == 1:
-        return "the same launch (N=1)"
+        return (f"same workload ({W}x{rc} at {spp} spp, N=1): committed PMC passes named in the *_source "
+                f"fields, another process; not this launch")
     return (f"per-rank launch: rows r::{world} at {spp} spp = {rc * W * spp / 1e6:.1f} M samples, the N=1 frame's "
-            f"workload within 1 %; evidence measured on the N=1 launch")
+            f"workload within 1 %; evidence: committed PMC passes of the N=1 workload named in the *_source fields")
 
 
 def traffic_per_launch(args, W, rc, spp):
@@ -148,17 +155,29 @@ def wf_traffic(args, W, rc, spp):
     except (OSError, ValueError):
         return None
     c = t.get("config", {})
-    fused = os.environ.get("RTW_WF_FUSED", "1") != "0"
+    fused = args.wf_form == "fused"
     if not same_per_rank_work(c, args, W, rc, spp) or args.wf_paths != 0 or c.get("fused", False) != fused \
-            or c.get("sets", 1) != wf_sets():
+            or c.get("sets", 1) != wf_sets(args) or args.wf_drain != "samples":
         return None
     return round(t["traffic_bytes_per_frame"])
 
 
-def wf_sets():
-    """Queue sets of the wavefront engine (RTW_WF_SETS, else the library default)."""
+def wf_sets(args):
+    """Queue sets of the wavefront engine (--wf-sets = params.wf_sets, else the library default)."""
     import rtw_amd as R
-    return int(os.environ.get("RTW_WF_SETS") or R.DEFAULT_WF_SETS)
+    return int(args.wf_sets or R.DEFAULT_WF_SETS)
+
+
+def wf_params(args):
+    """The wavefront engine's configuration fields of rtw_params (ABI v4)."""
+    return dict(wf_paths=args.wf_paths, wf_sets=args.wf_sets, wf_drain=args.wf_drain, wf_form=args.wf_form)
+
+
+def wf_kernels(args):
+    """The kernels one wavefront frame runs under this configuration."""
+    bounce = "wf_step" if args.wf_form == "fused" else "wf_extend + wf_shade"
+    drain = {"samples": " + wf_drain", "slots": " + wf_finish", "none": ""}[args.wf_drain]
+    return bounce + " (all bounce launches of one frame, every queue set)" + drain
 
 
 _CPU_CHILD = r"""
@@ -335,11 +354,11 @@ def world_variant(R, torch, scene, steps, warmup):
             "note": "world kernel, f64, bit-identical to oracle Tier B (tests/test_gpu_world.py)"}
 
 
-def wavefront_bytes(counts, precision, units):
+def wavefront_bytes(counts, precision, units, fused=True):
     """Algorithmic HBM bytes of one wavefront frame (rtw_wavefront.hip): per
     bounce segment of the fused engine (default), wf_step reads the path +
     its hit (root, winner) and writes the next path + its hit; of the split
-    engine (RTW_WF_FUSED=0), extend reads o, d, time (+ the skip word in f32)
+    engine (--wf-form split), extend reads o, d, time (+ the skip word in f32)
     and writes (root, winner), shade reads the path + (root, winner) and
     writes the path.  Per sample: the home slot's unit, sample index and f64x3 sum
     (read + write).  Per unit: the f64x3 chunk sum.  `counts` is the
@@ -348,7 +367,7 @@ def wavefront_bytes(counts, precision, units):
     load of each live path, <= 96 B x slots, is left out: < 0.1 %)."""
     r = 8 if precision == "f64" else 4
     path = 10 * r + 8 + 4 + 4
-    if os.environ.get("RTW_WF_FUSED", "1") != "0":  # fused engine: path + hit read, path + hit written
+    if fused:  # fused engine: path + hit read, path + hit written
         seg = 2 * (path + r + 4)
     else:  # extend reads o, d, time (+ skip), writes the hit; shade reads path + hit, writes the path
         seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
@@ -362,7 +381,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     tests/test_gpu_wavefront.py), timed the same way; roofline = HBM (the
     path queues stream through HBM every bounce)."""
     p = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
-                      precision=args.precision, engine="wavefront", wf_paths=args.wf_paths)
+                      precision=args.precision, engine="wavefront", **wf_params(args))
     counts = rend.counts(cam, p)  # untimed: the queue / in-register split of the segments
     torch.cuda.synchronize()
     w0 = time.perf_counter()
@@ -393,17 +412,17 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     sclk = clk.mhz()
     chunk = min(R.DEFAULT_CHUNK, spp)
     units = rc * W * ((spp + chunk - 1) // chunk)
-    byts = wavefront_bytes(counts, args.precision, units)
+    byts = wavefront_bytes(counts, args.precision, units, args.wf_form == "fused")
     gbs = byts / (ms * 1e-3) / 1e9
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
-            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(), "sclk_mhz": sclk,
+            "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
+            "wf_form": args.wf_form, "sclk_mhz": sclk,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
                          "evidence_scope": evidence_scope(world, W, rc, spp),
-                         "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
-                                   + " (all bounce launches of one frame, every queue set) + wf_drain",
+                         "kernel": wf_kernels(args),
                          "loop_ms_per_frame": round(ms, 3), "algorithmic_bytes_per_frame": byts,
                          "drain_segment_frac": round(drain, 4)},
             "note": "engine=wavefront (BASELINE configs[3]): per-bounce kernels over SoA path queues in HBM; "
@@ -543,7 +562,7 @@ def main():
     cam = R.cover_camera(ASPECT)
     rb, rs, rc = shard_rows(H, rank, world)
     params = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
-                           precision=args.precision, engine=args.engine, wf_paths=args.wf_paths)
+                           precision=args.precision, engine=args.engine, **wf_params(args))
     rend = TorchRenderer(sph, mats, local)
     out = torch.empty((rc, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
     samples_rank = rc * W * spp
@@ -643,12 +662,13 @@ def main():
                     "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
         }
     else:  # wavefront headline: HBM-bound path queues
-        byts = wavefront_bytes(rend.counts(cam, params), args.precision, rc * W * n_chunks)
+        byts = wavefront_bytes(rend.counts(cam, params), args.precision, rc * W * n_chunks, args.wf_form == "fused")
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
-                    "kernel": ("wf_step" if os.environ.get("RTW_WF_FUSED", "1") != "0" else "wf_extend + wf_shade")
-                                   + " (all bounce launches of one frame) + wf_finish",
+                    "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
+                    "evidence_scope": evidence_scope(world, W, rc, spp),
+                    "kernel": wf_kernels(args), "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
                     "loop_ms_per_frame": round(trace_ms_avg, 3), "algorithmic_bytes_per_frame": byts,
                     "valu": {"achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                              "frac": round(achieved_tf / peak, 4)}}
@@ -656,7 +676,7 @@ def main():
     extra = {}
     if not args.no_f32_variant and args.precision == "f64":
         p32 = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc, precision="f32",
-                            engine=args.engine, wf_paths=args.wf_paths)
+                            engine=args.engine, **wf_params(args))
         for _ in range(max(1, args.warmup)):
             rend.render(cam, p32, out=out)
         torch.cuda.synchronize()

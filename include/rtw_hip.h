@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 3
+#define RTW_ABI_VERSION 4
 
 typedef enum {
   RTW_OK = 0,
@@ -81,10 +81,26 @@ typedef enum {
 /* Render engine (both compute the same Tier-B image, bit for bit). */
 typedef enum {
   RTW_ENGINE_MEGAKERNEL = 0,  /* one persistent trace kernel (BASELINE.json configs[1]) */
-  RTW_ENGINE_WAVEFRONT = 1    /* per-bounce kernels over SoA path queues in HBM (configs[3]): one fused
-                                 shade + closest-hit kernel per bounce (env RTW_WF_FUSED=0: separate
-                                 extend / shade kernels; same image) */
+  RTW_ENGINE_WAVEFRONT = 1    /* per-bounce kernels over SoA path queues in HBM (configs[3]) */
 } rtw_engine;
+
+/* Wavefront engine, once the unit queue runs dry.  Every
+ * choice renders the same image, bit for bit. */
+typedef enum {
+  RTW_WF_DRAIN_SAMPLES = 0,   /* wf_drain: a segment's remaining samples dealt to its free lanes (default) */
+  RTW_WF_DRAIN_SLOTS = 1,     /* wf_finish: each lane runs its own slot's remaining samples */
+  RTW_WF_DRAIN_NONE = 2       /* no in-register drain: the bounce kernels' queues run to the end */
+} rtw_wf_drain;
+typedef enum {
+  RTW_WF_FUSED = 0,           /* one kernel per bounce: shade + the next closest hit (default) */
+  RTW_WF_SPLIT = 1            /* separate extend (closest hit) and shade kernels per bounce */
+} rtw_wf_form;
+
+/* World kernel instantiation (rtw_world_*; every choice gives the same bits). */
+typedef enum {
+  RTW_WORLD_FEATURES_AUTO = 0, /* the smallest compiled feature set holding the world's features */
+  RTW_WORLD_FEATURES_ALL = 1   /* the general kernel (every primitive, texture and transform) */
+} rtw_world_features;
 
 typedef struct {
   uint32_t width, height;     /* full image (main.zig:305-306) */
@@ -100,13 +116,24 @@ typedef struct {
   int32_t device;             /* HIP device for rtw_render (-1 = current) */
   uint32_t engine;            /* rtw_engine */
   uint32_t wf_paths;          /* wavefront: in-flight paths (queue capacity), 0 = RTW_DEFAULT_WF_PATHS */
+  /* ABI v4: engine configuration, all 0 = default.  The library reads no
+   * environment variable on the render path; rtw_workspace_bytes depends on
+   * these fields only. */
+  uint32_t wf_sets;           /* wavefront: independent queue sets (1-4), 0 = RTW_DEFAULT_WF_SETS */
+  uint32_t wf_drain;          /* wavefront: rtw_wf_drain */
+  uint32_t wf_form;           /* wavefront: rtw_wf_form */
+  uint32_t world_waves;       /* world kernel: register budget in waves per SIMD (1, 3 or 4),
+                                 0 = the feature set's default (4 sphere worlds, 3 rects / transforms, 2 noise) */
+  uint32_t world_features;    /* world kernel: rtw_world_features */
+  uint32_t reserved;          /* must be 0 */
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u
 #define RTW_DEFAULT_WF_PATHS (3u << 18) /* 786,432 in-flight paths (with two sets) */
 /* Wavefront queue sets: wf_paths is split over this many independent queue
- * sets, each driven on its own HIP stream (env RTW_WF_SETS overrides, 1-4). */
+ * sets, each driven on its own HIP stream (params.wf_sets overrides, 1-4). */
 #define RTW_DEFAULT_WF_SETS 2u
+#define RTW_MAX_WF_SETS 4u
 #define RTW_MAX_SPHERES 4096u
 
 /* ------------------------------------------------------------ queries -- */
@@ -183,10 +210,22 @@ int rtw_render_counts(rtw_scene scene, const rtw_camera *cam, const rtw_params *
                       void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
 /* The same pass with counts_out[6]: the four above, then the segments traced
  * and the samples finished by the wavefront engine's in-register drain
- * (wf_finish: paths that no longer stream through the HBM queues; 0 for the
- * megakernel and with RTW_WF_FINISH=0). */
+ * (paths that no longer stream through the HBM queues; 0 for the megakernel
+ * and with RTW_WF_DRAIN_NONE). */
 int rtw_render_counts_ex(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
                          void *workspace, size_t workspace_bytes, uint64_t counts_out[6]);
+/* The same pass with the kernels' raw statistics words (diagnostic):
+ * stats_out[RTW_STATS_WORDS], indices RTW_STAT_*. */
+#define RTW_STATS_WORDS 16
+enum {
+  RTW_STAT_SAMPLES = 0, RTW_STAT_SEGMENTS = 1, RTW_STAT_F32_SKIPS = 2,
+  RTW_STAT_CAND_WAVE_ITERS = 3, RTW_STAT_CAND_LANES = 4, RTW_STAT_DISC_GE0_LANES = 5,
+  RTW_STAT_SPHERE_LOOP_WAVE_ITERS = 6, RTW_STAT_CULL_SURVIVOR_LANES = 7, RTW_STAT_CULL_EXACT_WAVE_ITERS = 8,
+  RTW_STAT_DRAIN_SEGMENTS = 9, RTW_STAT_DRAIN_SAMPLES = 10, RTW_STAT_CLUSTER_WAVE_TESTS = 11,
+  RTW_STAT_CLUSTER_WAVE_SKIPS = 12, RTW_STAT_DRAIN_WAVE_ITERS = 13
+};
+int rtw_render_stats(rtw_scene scene, const rtw_camera *cam, const rtw_params *params,
+                     void *workspace, size_t workspace_bytes, uint64_t stats_out[RTW_STATS_WORDS]);
 
 /* =================================================== general worlds ===
  * Every other scene of the reference (main.zig:123-290) and BASELINE.json
@@ -286,8 +325,9 @@ int rtw_built_scene_free(rtw_built_scene b);
 
 /* Upload a world to the CURRENT device: tables + a BVH over worlds of more
  * than 32 primitives (flags bit 0 = RTW_WORLD_LINEAR: no BVH, every segment
- * tests every primitive in a wave-uniform loop). */
+ * tests every primitive in a wave-uniform loop; bit 1 = RTW_WORLD_DEBUG_BVH). */
 #define RTW_WORLD_LINEAR 1u
+#define RTW_WORLD_DEBUG_BVH 2u /* diagnostic: the BVH root's two children (leaf / node, boxes) to stderr */
 typedef struct rtw_world_s *rtw_world;
 int rtw_world_create(const rtw_world_desc *desc, uint32_t flags, rtw_world *out);
 int rtw_world_destroy(rtw_world world);
@@ -313,6 +353,11 @@ int rtw_world_render(const rtw_camera *cam, const rtw_world_desc *desc, const rt
 /* Statistics pass: counts_out[4] = {samples, segments, node_visits, prim_tests}. */
 int rtw_world_render_counts(rtw_world world, const rtw_camera *cam, const rtw_params *params,
                             void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
+/* The same pass with counts_out[6]: the four above, then the wave iterations
+ * of the persistent kernel and whether tail dealing ran (1: the workspace held
+ * the per-lane rings, 0: it did not — same image, slower end of launch). */
+int rtw_world_render_counts_ex(rtw_world world, const rtw_camera *cam, const rtw_params *params,
+                               void *workspace, size_t workspace_bytes, uint64_t counts_out[6]);
 
 #ifdef __cplusplus
 }

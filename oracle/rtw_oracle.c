@@ -617,14 +617,53 @@ void ro_main_cover(uint32_t W, double aspect, uint32_t spp, uint32_t depth, uint
 /* Tier B: the GPU contract (per-sample counter-keyed Xoshiro256++)        */
 /* ===================================================================== */
 
-/* Tier-B RNG: Zig std.Random.SplitMix64 used as a COUNTER-BASED generator.
- * base = SplitMix64.init(seed).next(); sample (pixel p, sample s) owns the
- * disjoint block of 2^16 consecutive Weyl states starting at
+/* Tier-B RNG: a COUNTER-BASED generator over SplitMix64's Weyl sequence.
+ * base = SplitMix64.init(seed).next() (std/Random/SplitMix64.zig, as
+ * Tier A's seeding); sample (pixel p, sample s) owns the disjoint block of
+ * 2^16 consecutive Weyl states starting at
  *   base + (((p << 24) | s) << 16) * gamma,
- * i.e. its stream is SplitMix64.init(that state).next(), next(), ...  Every
- * draw of a frame is a distinct element of ONE SplitMix64 sequence (gamma is
- * odd, so n -> n*gamma is a bijection), any draw is computable from
- * (p, s, k) alone, and u64 -> f64/f32 is Zig's Random.float as in Tier A. */
+ * and its draws are ro_tb_mix of the next states: draw k of the sample is
+ * ro_tb_mix(that state + (k + 1) * gamma).  Every draw of a frame is the mix
+ * of a distinct element of ONE Weyl sequence (gamma is odd, so n -> n*gamma
+ * is a bijection), any draw is computable from (p, s, k) alone, and
+ * u64 -> f64/f32 is Zig's Random.float as in Tier A.
+ *
+ * The mixer (round 5; rounds 1-4 used SplitMix64's own output function,
+ * ro_splitmix64_next's last three lines): four Feistel half-rounds on the
+ * state's 32-bit words (hi, lo), each a 32x32 -> 64-bit product and one xor:
+ *   t = hi * M0; lo ^= t >> 32; hi = (uint32)t;   then lo * M1 into hi,
+ *   hi * M2 into lo, lo * M3 into hi.
+ * It is a bijection of the 64-bit state.  The reference renders with ONE
+ * sequential Xoshiro256++ stream (main.zig:300), which no parallel renderer
+ * can reproduce, so Tier B's only requirement on the mixer is statistical:
+ * tests/native/rng_stats.c (mixer 10) checks bit bias, byte uniformity,
+ * lag-1/2/3 pairs and triples of one sample's draws, and every byte of the
+ * draws of neighbouring samples and pixels over 2^32 draws laid out as a
+ * render uses them (tests/test_rng_stats.py); Tier C checks
+ * the image against Tier A's. */
+uint64_t ro_tb_mix(uint64_t z) {
+  static const uint32_t M[4] = {0xD2511F53u, 0xCD9E8D57u, 0x9E3779B1u, 0x85EBCA6Bu};
+  uint32_t hi = (uint32_t)(z >> 32), lo = (uint32_t)z;
+  uint64_t t;
+  t = (uint64_t)hi * M[0];
+  lo ^= (uint32_t)(t >> 32);
+  hi = (uint32_t)t;
+  t = (uint64_t)lo * M[1];
+  hi ^= (uint32_t)(t >> 32);
+  lo = (uint32_t)t;
+  t = (uint64_t)hi * M[2];
+  lo ^= (uint32_t)(t >> 32);
+  hi = (uint32_t)t;
+  t = (uint64_t)lo * M[3];
+  hi ^= (uint32_t)(t >> 32);
+  lo = (uint32_t)t;
+  return ((uint64_t)hi << 32) | lo;
+}
+static inline uint64_t tb_next(uint64_t *st) {
+  *st += 0x9e3779b97f4a7c15ULL;
+  return ro_tb_mix(*st);
+}
+
 static inline uint64_t tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample) {
   uint64_t sm = seed;
   const uint64_t base = ro_splitmix64_next(&sm);
@@ -636,18 +675,19 @@ static inline uint64_t tierb_state(uint64_t seed, uint64_t pixel, uint64_t sampl
  * change that makes every draw exactly one Weyl step (so draw k of a sample is
  * random-access): when the draw's u64 has >= 12 (f64) / >= 41 (f32) leading
  * zeros, Zig takes further u64s from the same generator; here they come from
- * the draw's own extension stream SplitMix64.init(state_of_draw ^ kTierBExt).
- * Probability 2^-12 / 2^-41 per draw; the value distribution is unchanged. */
+ * the draw's own extension stream: the Weyl sequence from state_of_draw ^
+ * kTierBExt through the same mixer.  Probability 2^-12 / 2^-41 per draw; the
+ * value distribution is unchanged. */
 #define kTierBExt 0x5851F42D4C957F2DULL
 
 double ro_sm_f64(uint64_t *st) {
-  const uint64_t rnd = ro_splitmix64_next(st);
+  const uint64_t rnd = tb_next(st);
   uint64_t lz = clz64(rnd);
   if (lz >= 12) {
     uint64_t ext = *st ^ kTierBExt;
     lz = 12;
     for (;;) {
-      const uint64_t addl = clz64(ro_splitmix64_next(&ext));
+      const uint64_t addl = clz64(tb_next(&ext));
       lz += addl;
       if (addl != 64) break;
       if (lz >= 1022) { lz = 1022; break; }
@@ -660,13 +700,13 @@ double ro_sm_f64(uint64_t *st) {
 }
 
 float ro_sm_f32(uint64_t *st) {
-  const uint64_t rnd = ro_splitmix64_next(st);
+  const uint64_t rnd = tb_next(st);
   uint32_t lz = clz64(rnd);
   if (lz >= 41) {
     uint64_t ext = *st ^ kTierBExt;
-    lz = 41 + clz64(ro_splitmix64_next(&ext));
+    lz = 41 + clz64(tb_next(&ext));
     if (lz == 41 + 64) {
-      const uint32_t r32 = (uint32_t)ro_splitmix64_next(&ext) | 0x7FFu;
+      const uint32_t r32 = (uint32_t)tb_next(&ext) | 0x7FFu;
       lz += (uint32_t)__builtin_clz(r32);
     }
   }

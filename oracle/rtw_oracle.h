@@ -98,6 +98,7 @@ float ro_random_f32(uint64_t s[4]);
 
 /* Tier-B counter-based stream (see rtw_oracle.c tierb_state). */
 uint64_t ro_tierb_state(uint64_t seed, uint64_t pixel, uint64_t sample);
+uint64_t ro_tb_mix(uint64_t weyl_state); /* the draw's u64 (Feistel mixer) */
 double ro_sm_f64(uint64_t *state);
 float ro_sm_f32(uint64_t *state);
 

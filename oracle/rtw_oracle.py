@@ -84,6 +84,8 @@ def lib():
         L.ro_random_f32.argtypes = [U64x4]
         L.ro_tierb_state.restype = C.c_uint64
         L.ro_tierb_state.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        L.ro_tb_mix.restype = C.c_uint64
+        L.ro_tb_mix.argtypes = [C.c_uint64]
         L.ro_sm_f64.restype = C.c_double
         L.ro_sm_f64.argtypes = [C.POINTER(C.c_uint64)]
         L.ro_sm_f32.restype = C.c_float

@@ -29,6 +29,23 @@ class SplitMix64:  # std/Random/SplitMix64.zig
         return z ^ (z >> 31)
 
 
+def tb_mix(z):
+    """Tier-B draw word of a Weyl state (the GPU contract, not the reference:
+    oracle/rtw_oracle.c ro_tb_mix): four Feistel half-rounds on the 32-bit
+    words, each a 32x32 -> 64-bit product and one xor."""
+    hi, lo = (z >> 32) & 0xFFFFFFFF, z & 0xFFFFFFFF
+    for i, m in enumerate((0xD2511F53, 0xCD9E8D57, 0x9E3779B1, 0x85EBCA6B)):
+        if i % 2 == 0:
+            t = hi * m
+            lo ^= t >> 32
+            hi = t & 0xFFFFFFFF
+        else:
+            t = lo * m
+            hi ^= t >> 32
+            lo = t & 0xFFFFFFFF
+    return (hi << 32) | lo
+
+
 def _rotl(x, k):
     return ((x << k) | (x >> (64 - k))) & M64
 

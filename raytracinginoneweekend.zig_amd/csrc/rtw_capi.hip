@@ -40,6 +40,18 @@ int fail(int status, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(RTW_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// Development knobs (tools/, A/B measurement) are read from the environment
+// only in the -DRTW_MEASURE build; the product library's behaviour depends on
+// its arguments alone (engine configuration: rtw_params, ABI v4).
+const char* dev_knob(const char* name) {
+#ifdef RTW_MEASURE
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 uint64_t splitmix_first(uint64_t seed) {  // SplitMix64.init(seed).next()
   uint64_t z = seed + 0x9e3779b97f4a7c15ULL;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -83,7 +95,7 @@ int wf_bpc(int dev, int prec, int kernel, size_t lds) {
 // RTW_VARIANT selects another one of a -DRTW_MEASURE build (tools/); a value
 // that was not compiled in is refused by launch_all.
 int kernel_variant(uint32_t precision) {
-  const char* v = getenv("RTW_VARIANT");
+  const char* v = dev_knob("RTW_VARIANT");
   if (v && *v) return atoi(v);
   return precision == RTW_PRECISION_F32 ? rtwk::kDefaultVarF32 : rtwk::kDefaultVarF64;
 }
@@ -498,6 +510,12 @@ int validate(const rtw_params* p) {
                 p->row_count, p->height);
   if (p->precision > RTW_PRECISION_F32) return fail(RTW_EINVAL, "precision %u", p->precision);
   if (p->engine > RTW_ENGINE_WAVEFRONT) return fail(RTW_EINVAL, "engine %u", p->engine);
+  if (p->wf_sets > RTW_MAX_WF_SETS) return fail(RTW_EINVAL, "wf_sets %u outside [0, %u]", p->wf_sets, RTW_MAX_WF_SETS);
+  if (p->wf_drain > RTW_WF_DRAIN_NONE) return fail(RTW_EINVAL, "wf_drain %u", p->wf_drain);
+  if (p->wf_form > RTW_WF_SPLIT) return fail(RTW_EINVAL, "wf_form %u", p->wf_form);
+  if (p->world_waves > 4) return fail(RTW_EINVAL, "world_waves %u outside [0, 4]", p->world_waves);
+  if (p->world_features > RTW_WORLD_FEATURES_ALL) return fail(RTW_EINVAL, "world_features %u", p->world_features);
+  if (p->reserved != 0) return fail(RTW_EINVAL, "params.reserved must be 0");
   if (p->engine == RTW_ENGINE_WAVEFRONT && (p->wf_paths > (1u << 28) || (p->wf_paths && p->wf_paths < 64)))
     return fail(RTW_EINVAL, "wf_paths %u outside [64, 2^28]", p->wf_paths);
   if (p->engine == RTW_ENGINE_WAVEFRONT && p->max_depth > 0xFFFFu)
@@ -511,31 +529,25 @@ int validate(const rtw_params* p) {
   return RTW_OK;
 }
 
-// Wavefront queue sets (RTW_WF_SETS, default kWfSets): the in-flight paths
+// Wavefront queue sets (params.wf_sets, default kWfSets): the in-flight paths
 // are split over independent sets (queues, home slots, segment counts,
 // reservoirs, drain ring), each driven on its own HIP stream, so one set's
 // launch ramps, tails and drain overlap the other sets' bounce launches.  All
 // sets take units from the one device queue: a unit belongs to one slot of
 // one set, its chunk sum keeps its sample order, the image keeps its bits.
-constexpr uint32_t kWfMaxSets = 4;
+constexpr uint32_t kWfMaxSets = RTW_MAX_WF_SETS;
 constexpr uint32_t kWfSets = RTW_DEFAULT_WF_SETS;
-uint32_t wf_sets() {
-  const char* e = getenv("RTW_WF_SETS");
-  const int v = (e && *e) ? atoi(e) : (int)kWfSets;
-  return (uint32_t)std::min<int>(std::max(v, 1), (int)kWfMaxSets);
-}
-// The in-register drain: wf_drain (samples dealt to the wave's free lanes,
-// default) or wf_finish (RTW_WF_DRAIN=0: a lane runs its own slot's samples).
-// Only wf_drain uses the drain ring, so only it reserves one.
-bool wf_per_sample_drain() {
-  const char* de = getenv("RTW_WF_DRAIN");
-  return !(de && *de == '0');
-}
+uint32_t wf_sets(const rtw_params* p) { return p->wf_sets ? p->wf_sets : kWfSets; }  // (validated: 1-4)
+// The in-register drain (params.wf_drain): wf_drain (RTW_WF_DRAIN_SAMPLES,
+// samples dealt to the wave's free lanes, default), wf_finish
+// (RTW_WF_DRAIN_SLOTS: a lane runs its own slot's samples) or none.  Only
+// wf_drain uses the drain ring, so only it reserves one.
+bool wf_per_sample_drain(const rtw_params* p) { return p->wf_drain == RTW_WF_DRAIN_SAMPLES; }
 // Segments of one queue set: its share of wf_paths rounded up to whole
 // segments (one per wave).
 uint32_t wf_segs(const rtw_params* p) {
   const uint32_t n = p->wf_paths ? p->wf_paths : RTW_DEFAULT_WF_PATHS;
-  const uint32_t per_set = (n + wf_sets() - 1) / wf_sets();
+  const uint32_t per_set = (n + wf_sets(p) - 1) / wf_sets(p);
   return std::max(1u, (per_set + rtwk::kSegCap - 1) / rtwk::kSegCap);
 }
 
@@ -566,16 +578,16 @@ WsLayout ws_layout(const rtw_params* p) {
     const size_t r = p->precision == RTW_PRECISION_F32 ? 4 : 8;
     w.wf_set_bytes = 2 * wf_queue_bytes(n, r) + al256(n * r) + al256(n * 4) + al256(n * sizeof(rtwk::HomeRec)) +
                      2 * al256(segs * 4) + al256(segs * 8) +
-                     (wf_per_sample_drain() ? al256(n * rtwk::kDrainWin * 3 * r) : 0);
-    w.total += wf_sets() * w.wf_set_bytes;
+                     (wf_per_sample_drain(p) ? al256(n * rtwk::kDrainWin * 3 * r) : 0);
+    w.total += wf_sets(p) * w.wf_set_bytes;
   }
   return w;
 }
 
-// Unit dealing order (rtw_device.hpp dealt_unit): RTW_UNIT_ORDER=fwd|rev
-// overrides the engine's default.
+// Unit dealing order (rtw_device.hpp dealt_unit): the development knob
+// RTW_UNIT_ORDER=fwd|rev overrides the engine's default (-DRTW_MEASURE only).
 uint32_t unit_order(uint32_t dflt) {
-  const char* uo = getenv("RTW_UNIT_ORDER");
+  const char* uo = dev_knob("RTW_UNIT_ORDER");
   if (uo && std::strcmp(uo, "fwd") == 0) return 0u;
   if (uo && std::strcmp(uo, "rev") == 0) return 1u;
   return dflt;
@@ -734,12 +746,31 @@ uint32_t* poll_words() {
 }
 
 // Side streams of the wavefront queue sets 1.. (set 0 runs on the caller's
-// stream), created once per device and thread; non-blocking, joined to the
-// caller's stream by events on every render.
+// stream): created once per device for the whole process (not per host
+// thread, so a process does not accumulate streams beyond the hardware
+// queues, where HIP would map them round-robin onto shared queues and a set
+// could land on its caller's queue — correct, but serial); non-blocking,
+// joined to the caller's stream by events on every render; destroyed at
+// library teardown.  Concurrent wavefront renders on one device from several
+// threads share them (stream-ordered: still correct).
+struct SideStreams {
+  std::mutex mu;
+  std::map<std::pair<int, uint32_t>, hipStream_t> s;
+  ~SideStreams() {
+    for (auto& kv : s)
+      if (kv.second) (void)hipStreamDestroy(kv.second);
+  }
+};
+SideStreams g_side;
 hipStream_t wf_side_stream(int dev, uint32_t k) {
-  thread_local std::map<std::pair<int, uint32_t>, hipStream_t> streams;
-  hipStream_t& s = streams[{dev, k}];
-  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  std::lock_guard<std::mutex> lk(g_side.mu);
+  hipStream_t& s = g_side.s[{dev, k}];
+  if (!s) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur != dev ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+      s = nullptr;
+  }
   return s;
 }
 
@@ -774,33 +805,34 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     HIP_TRY(hipMemsetAsync(ws + L.partial_off, 0, L.partial_bytes, stream));
     return RTW_OK;
   }
-  const uint32_t segs = wf_segs(p), nsets = wf_sets();
+  const uint32_t segs = wf_segs(p), nsets = wf_sets(p);
   const size_t n = (size_t)segs * rtwk::kSegCap;
-  const bool per_sample = wf_per_sample_drain();
-  // Units per reservoir refill (RTW_WF_BATCH, default kWfBatch): the refills'
-  // atomics against the work a reservoir still holds when the queue runs dry.
-  const char* be = getenv("RTW_WF_BATCH");
+  const bool per_sample = wf_per_sample_drain(p);
+  // Units per reservoir refill (kWfBatch; development knob RTW_WF_BATCH): the
+  // refills' atomics against the work a reservoir still holds when the queue
+  // runs dry.
+  const char* be = dev_knob("RTW_WF_BATCH");
   const uint32_t refill = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
   // Persistent grids: every resident wave slot of each bounce kernel (at most
   // one wave per segment); the same grids for every launch of the frame.
-  // The drains run one wave per segment (wf_drain has no segment loop).
+  // The drains always run max_grid = ceil(segs / waves per block) blocks: one
+  // wave per segment (wf_drain has no segment loop; grid_of never sizes them).
   const uint32_t max_grid = (segs + rtwk::kTraceBlock / 64 - 1) / (rtwk::kTraceBlock / 64);
-  if ((uint64_t)max_grid * (rtwk::kTraceBlock / 64) < segs) return fail(RTW_EINVAL, "drain grid below one wave per segment");
   // RTW_WF_GRID (development knob): N > 0 = N x the resident grid, capped at one wave per segment.
-  const char* gk = getenv("RTW_WF_GRID");
+  const char* gk = dev_knob("RTW_WF_GRID");
   const uint32_t gmul = (gk && *gk) ? (uint32_t)std::max(1, atoi(gk)) : 1u;
   // RTW_WF_SET_GRID (development knob): each set's bounce grid = the resident grid / N.
-  const char* sg = getenv("RTW_WF_SET_GRID");
+  const char* sg = dev_knob("RTW_WF_SET_GRID");
   const uint32_t gdiv = (sg && *sg) ? (uint32_t)std::max(1, atoi(sg)) : 1u;
   auto grid_of = [&](int kernel) {
     const uint32_t per_cu = (uint32_t)wf_bpc(dev, (int)(sizeof(R) == 4), kernel, lds);
     return std::max(1u, std::min((uint32_t)device_cus(dev) * per_cu * gmul / gdiv, max_grid));
   };
   const uint32_t grid = grid_of(2), grid_ext = grid_of(1), grid_step = grid_of(3);
-  // Fused engine (default; RTW_WF_FUSED=0: separate extend and shade kernels):
-  // one kernel per bounce, the closest hit computed where the ray is made.
-  const char* fz = getenv("RTW_WF_FUSED");
-  const bool fused = !(fz && *fz == '0');
+  // Fused engine (default; params.wf_form RTW_WF_SPLIT: separate extend and
+  // shade kernels): one kernel per bounce, the closest hit computed where the
+  // ray is made.
+  const bool fused = p->wf_form == RTW_WF_FUSED;
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
   WfSet<R> set[kWfMaxSets];
@@ -854,16 +886,17 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // Termination bound (never reached by a correct kernel): every iteration
   // advances every live path by one segment.
   const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / kWfIters + 4;
-  // Wall-clock guard as well (RTW_WF_TIMEOUT_S, default 300 s): a queue that
-  // never drains is reported instead of hanging the caller.
-  const char* tos = getenv("RTW_WF_TIMEOUT_S");
+  // Wall-clock guard as well (300 s; development knob RTW_WF_TIMEOUT_S): a
+  // queue that never drains is reported instead of hanging the caller.
+  const char* tos = dev_knob("RTW_WF_TIMEOUT_S");
   const double timeout_s = (tos && *tos) ? atof(tos) : 300.0;
   const auto t_start = std::chrono::steady_clock::now();
-  // Drain in registers once a set's polled live count falls below
-  // RTW_WF_FINISH x its slots (default 1: as soon as slots start to retire,
-  // i.e. the unit queue ran dry; 0 = drain through the queues to the end).
-  const char* fe = getenv("RTW_WF_FINISH");
-  const double fin_frac = (fe && *fe) ? atof(fe) : 1.0;
+  // Drain in registers once a set's polled live count falls below fin_frac x
+  // its slots: 1 as soon as slots start to retire, i.e. the unit queue ran
+  // dry; 0 with RTW_WF_DRAIN_NONE (through the queues to the end); the
+  // development knob RTW_WF_FINISH sets another fraction.
+  const char* fe = dev_knob("RTW_WF_FINISH");
+  const double fin_frac = p->wf_drain == RTW_WF_DRAIN_NONE ? 0.0 : (fe && *fe) ? atof(fe) : 1.0;
   uint32_t left = st == RTW_OK ? nsets : 0u;
   while (left > 0 && st == RTW_OK) {
     // Enqueue one batch on every running set, then look at each set's
@@ -1109,13 +1142,16 @@ int rtw_render_device(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, 
   return launch_all(sc, cam, p, workspace, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, 0);
 }
 
-int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
-                         size_t ws_bytes, uint64_t counts_out[6]) {
-  if (!sc || !cam || !counts_out) return fail(RTW_EINVAL, "scene/camera/counts is NULL");
+// The statistics pass: one render in counting mode, the kernels' 32 statistics
+// words copied back (rtw_hip.h RTW_STAT_*; words 16.. are the diagnostic
+// build's phase stamps).
+static int stats_pass(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace, size_t ws_bytes,
+               unsigned long long (&st)[32]) {
+  if (!sc || !cam) return fail(RTW_EINVAL, "scene/camera is NULL");
   const int v = validate(p);
   if (v != RTW_OK) return v;
   // RTW_PHASE_PROFILE=1: diagnostic build with per-phase s_memtime stamps.
-  const char* prof = getenv("RTW_PHASE_PROFILE");
+  const char* prof = dev_knob("RTW_PHASE_PROFILE");
   const int mode = (prof && prof[0] == '1') ? 2 : 1;
 #ifndef RTW_MEASURE
   if (mode == 2) return fail(RTW_UNSUPPORTED, "RTW_PHASE_PROFILE needs the -DRTW_MEASURE build (tools/gpu_phase.sh)");
@@ -1123,10 +1159,10 @@ int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* 
   const int r = launch_all(sc, cam, p, workspace, ws_bytes, nullptr, nullptr, nullptr, nullptr, mode);
   if (r != RTW_OK) return r;
   HIP_TRY(hipDeviceSynchronize());
-  unsigned long long st[32] = {0};
+  for (auto& x : st) x = 0;
   const WsLayout L = ws_layout(p);
   HIP_TRY(hipMemcpy(st, static_cast<unsigned char*>(workspace) + L.stats_off, sizeof(st), hipMemcpyDeviceToHost));
-  if (mode == 1 && getenv("RTW_COUNTS_VERBOSE")) {
+  if (mode == 1 && dev_knob("RTW_COUNTS_VERBOSE")) {
     fprintf(stderr, "[rtw counts] samples %llu segments %llu skipped %llu cand_wave_iters %llu cand_lanes %llu "
             "disc_ge0_lanes %llu sphere_loop_wave_iters %llu cull_survivor_lanes %llu cull_exact_wave_iters %llu "
             "cluster_wave_tests %llu cluster_wave_skips %llu\n", st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8],
@@ -1144,6 +1180,25 @@ int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* 
       fprintf(stderr, "[rtw phase] %-15s %6.2f%%  (%llu wave-cycles)\n", names[i], tot ? 100.0 * st[16 + i] / tot : 0.0,
               st[16 + i]);
   }
+  return RTW_OK;
+}
+
+int rtw_render_stats(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace, size_t ws_bytes,
+                     uint64_t stats_out[RTW_STATS_WORDS]) {
+  if (!stats_out) return fail(RTW_EINVAL, "stats is NULL");
+  unsigned long long st[32];
+  const int r = stats_pass(sc, cam, p, workspace, ws_bytes, st);
+  if (r != RTW_OK) return r;
+  for (int i = 0; i < RTW_STATS_WORDS; ++i) stats_out[i] = st[i];
+  return RTW_OK;
+}
+
+int rtw_render_counts_ex(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* workspace,
+                         size_t ws_bytes, uint64_t counts_out[6]) {
+  if (!counts_out) return fail(RTW_EINVAL, "counts is NULL");
+  unsigned long long st[32];
+  const int r = stats_pass(sc, cam, p, workspace, ws_bytes, st);
+  if (r != RTW_OK) return r;
   counts_out[0] = st[0];
   counts_out[1] = st[1];
   // every segment tests every sphere; f32 mode skips one small sphere per segment with a skip set
@@ -1223,6 +1278,7 @@ int rtw_fail(int status, const char* fmt, ...) {
   return fail(status, "%s", buf);
 }
 int rtw_validate_params(const rtw_params* p) { return validate(p); }
+const char* rtw_dev_knob(const char* name) { return dev_knob(name); }
 size_t rtw_ws_total(const rtw_params* p) { return ws_layout(p).total; }
 size_t rtw_ws_stats_off(const rtw_params* p) { return ws_layout(p).stats_off; }
 size_t rtw_ws_counter_off(const rtw_params* p) { return ws_layout(p).counter_off; }

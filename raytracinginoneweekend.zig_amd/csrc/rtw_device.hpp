@@ -114,19 +114,17 @@ __device__ __forceinline__ uint32_t dealt_unit(uint32_t raw, const A& a) {
 }
 
 // ------------------------------------------------------------------ RNG --
-// Counter-based Zig std.Random.SplitMix64: sample (pixel p, sample s) owns the
-// 2^16 Weyl states starting at base + (((p << 24) | s) << 16) * gamma; its
-// draws are SplitMix64.next() from there, turned into reals by Zig's
-// Random.float (oracle/rtw_oracle.c tierb_state / ro_sm_f64 / ro_sm_f32).
+// Counter-based Tier-B generator over SplitMix64's Weyl sequence: sample
+// (pixel p, sample s) owns the 2^16 Weyl states starting at
+// base + (((p << 24) | s) << 16) * gamma; its draws are the mixer sm_mix of
+// the next states, turned into reals by Zig's Random.float
+// (oracle/rtw_oracle.c tierb_state / ro_tb_mix / ro_sm_f64 / ro_sm_f32).
 // Every draw is exactly one Weyl step: the rare extra words Random.float needs
-// for a tiny value come from the draw's own extension stream
-// SplitMix64.init(state ^ kExt), so draw k of a block sits at state
+// for a tiny value come from the draw's own extension stream (the Weyl states
+// from state ^ kExt, same mixer), so draw k of a block sits at state
 // W + (k + 1) * gamma and any lane can evaluate any draw (coop_reject).
 constexpr uint64_t kGamma = 0x9e3779b97f4a7c15ULL;
 constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
-#ifndef RTW_MUL64_MAD
-#define RTW_MUL64_MAD 1  // (A/B: 0 = the C multiply; profiles/r04/mul64_mad_ab.txt)
-#endif
 // z * c mod 2^64 on 32-bit lanes as three chained v_mad_u64_u32: the low
 // product lo*c_lo, then the high word accumulated as lo32(hi*c_lo + ph) and
 // lo32(lo*c_hi + that) (the laundering keeps each mad 64-bit, which the
@@ -134,7 +132,6 @@ constexpr uint64_t kExt = 0x5851F42D4C957F2DULL;
 // instructions per product).  Same bits as the C multiply.
 template <uint64_t C>
 __device__ __forceinline__ uint64_t mul64c(uint64_t z) {
-#if RTW_MUL64_MAD
   const uint32_t lo = (uint32_t)z, hi = (uint32_t)(z >> 32);
   const uint64_t p = (uint64_t)lo * (uint32_t)C;
   uint64_t q = (uint64_t)hi * (uint32_t)C + (p >> 32);
@@ -144,9 +141,6 @@ __device__ __forceinline__ uint64_t mul64c(uint64_t z) {
   uint64_t r = (uint64_t)lo * (uint32_t)(C >> 32) + q;
   asm("" : "+v"(r));
   return (r << 32) | (uint32_t)p;
-#else
-  return z * C;
-#endif
 }
 // z ^ (z >> k): one v_lshrrev_b64 + two v_xor_b32 (from 32-bit v_alignbit /
 // shift / xor instead: 1.3 % slower, profiles/r04/xsh32_scalar_decide_ab.txt)
@@ -154,10 +148,45 @@ template <int K>
 __device__ __forceinline__ uint64_t xsh(uint64_t z) {
   return z ^ (z >> K);
 }
+#ifndef RTW_RNG_MIX
+#define RTW_RNG_MIX 10
+#endif
+#if RTW_RNG_MIX != 10 && !defined(RTW_MEASURE)
+#error "RTW_RNG_MIX other than 10 (the Tier-B contract) exists only in the -DRTW_MEASURE build (A/B timing)"
+#endif
+// One Feistel half-round on the state's 32-bit words: t = x * M as ONE
+// v_mad_u64_u32 (the full 64-bit product), the other word ^= hi(t), x = lo(t).
+template <uint32_t M>
+__device__ __forceinline__ void feistel(uint32_t& x, uint32_t& y) {
+  const uint64_t t = (uint64_t)x * M;
+  y ^= (uint32_t)(t >> 32);
+  x = (uint32_t)t;
+}
+// The Tier-B mixer of a Weyl state (oracle/rtw_oracle.c ro_tb_mix).
+//  10 (the contract since round 5): four Feistel half-rounds, the first on the
+//     high word — 4 v_mad_u64_u32 + 4 v_xor_b32 (tests/native/rng_stats.c
+//     mixer 10: passes the battery over 2^32 draws of the render's layout);
+//   0: Zig's SplitMix64 (rounds 1-4): 2 x (3 v_mad_u64_u32) + 3 x 64-bit
+//     xorshift;  1: its 32-bit-fold form (MurmurHash3 fmix64 with >> 32).
 __device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
+#if RTW_RNG_MIX == 10
+  uint32_t a = (uint32_t)(z >> 32), b = (uint32_t)z;
+  feistel<0xD2511F53u>(a, b);
+  feistel<0xCD9E8D57u>(b, a);
+  feistel<0x9E3779B1u>(a, b);
+  feistel<0x85EBCA6Bu>(b, a);
+  return ((uint64_t)a << 32) | b;
+#elif RTW_RNG_MIX == 1
+  z = mul64c<0xff51afd7ed558ccdULL>(xsh<32>(z));
+  z = mul64c<0xc4ceb9fe1a85ec53ULL>(xsh<32>(z));
+  return xsh<32>(z);
+#elif RTW_RNG_MIX == 2  // (measurement only: fails the battery's neighbour-pixel tests)
+  return xsh<32>(mul64c<0xd6e8feb86659fd93ULL>(xsh<32>(z)));
+#else
   z = mul64c<0xbf58476d1ce4e5b9ULL>(xsh<30>(z));
   z = mul64c<0x94d049bb133111ebULL>(xsh<27>(z));
   return xsh<31>(z);
+#endif
 }
 __device__ __forceinline__ uint64_t sm_next(uint64_t& st) {
   st += kGamma;

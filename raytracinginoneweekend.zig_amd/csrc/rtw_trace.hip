@@ -31,15 +31,12 @@
 
 #include "rtw_device.hpp"
 
-#ifndef RTW_TRACE_LANE_FLAGS
-// The lane's state flags (have_unit, have_ray, done, shading) as bits of one
+// (Round 4) The lane's state flags (have_unit, have_ray, done, shading) as bits of one
 // u32 (rtw_device.hpp LaneFlag) instead of bools: as bools they were 64-bit
 // lane masks in SGPRs for the whole loop, and at the 100-SGPR limit the loop
 // spilled SGPRs to VGPR lanes and one 8-B pair to scratch.  Hot loop: 14 -> 6
 // lane ops, 2 -> 1 scratch pairs; -1.4 % per configs[1] frame
-// (profiles/r04/trace_lane_flags_ab.txt).  0: bools.
-#define RTW_TRACE_LANE_FLAGS 1
-#endif
+// (profiles/r04/trace_lane_flags_ab.txt).
 
 namespace rtwk {
 
@@ -94,16 +91,10 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   L.sx = L.sy = L.sz = 0.0;
   L.rs = 0;
   L.skip = -1;
-#if RTW_TRACE_LANE_FLAGS
   uint32_t lane_flags = 0u;  // (rtw_device.hpp LaneFlag)
   LaneFlag<1u> have_unit{lane_flags};
   LaneFlag<2u> have_ray{lane_flags};
   LaneFlag<4u> done{lane_flags};
-#else
-  bool have_unit = false;  // lane owns a (pixel, chunk) unit
-  bool have_ray = false;   // lane has a live path
-  bool done = false;       // queue exhausted for this lane
-#endif
   uint32_t qnext = 0, qend = 0;  // wave-uniform batch [qnext, qend)
   KStats st;
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
@@ -260,11 +251,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     // hit].  A lane whose path missed starts its next sample in the next
     // iteration before that iteration's closest hit, as in the default loop;
     // each sample's draws are in the reference's order.
-#if RTW_TRACE_LANE_FLAGS
     LaneFlag<8u> shading{lane_flags};
-#else
-    bool shading = false;
-#endif
     uint32_t kind = 0;
     int hit = -1;
     R tmax = kInf;

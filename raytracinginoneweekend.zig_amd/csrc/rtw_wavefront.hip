@@ -27,9 +27,6 @@
 
 #include "rtw_device.hpp"
 
-#ifndef RTW_RING_FENCE_WG
-#define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the drain's ring)
-#endif
 
 namespace rtwk {
 
@@ -382,11 +379,7 @@ __global__ void __launch_bounds__(kTraceBlock, kWfExtendOcc) wf_extend(WfArgs<R>
     if (cur_ok) {
       int hit = -1;
       R tmax = (R)__builtin_huge_val();
-#ifdef RTW_WF_EXT_LEGACY
-      closest_hit<R, F32, 0, 0>(S, T, cur, tmin, pre_k, lid, st, hit, tmax);
-#else
       closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, cur, tmin, pre_k, lid, st, hit, tmax);
-#endif
       const uint32_t i = seg * kSegCap + lid;
       A.hit_t[i] = tmax;
       A.hit_k[i] = hit;
@@ -451,14 +444,11 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
 #ifndef RTW_WF_STEP_OCC
 #define RTW_WF_STEP_OCC 5  // profiles/r02/wf_step_ab.txt: 5 waves (32-B spill) ~3 % faster than 4
 #endif
-#ifndef RTW_WF_KARG
 // wf_step / wf_drain read their arguments through the kernarg pointer where
 // used: held in SGPRs for the whole kernel (30 queue pointers among them) they
 // were spilled to VGPR lanes around the closest hit (wf_step 93 -> 34,
 // wf_drain 291 -> 93 v_readlane / v_writelane); -0.6 to -0.9 % per wavefront
-// frame (profiles/r04/wf_karg_ab.txt).  0: the by-value argument.
-#define RTW_WF_KARG 1
-#endif
+// frame (profiles/r04/wf_karg_ab.txt).
 // The kernel's argument (WfArgs, at offset 0 of the kernarg segment) through
 // a pointer the compiler cannot see through (rtw_device.hpp opaque): its
 // fields are scalar-loaded where used instead of held in SGPRs.
@@ -467,9 +457,9 @@ __device__ __forceinline__ const WfArgs<R>& wkargs() {
   return *(const WfArgs<R>*)opaque((const RTW_CONST WfArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr());
 }
 template <typename R, bool F32, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step(WfArgs<R> A_arg) {
+__global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_unused]] WfArgs<R> A_arg) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  const WfArgs<R>& A = RTW_WF_KARG ? wkargs<R>() : A_arg;
+  const WfArgs<R>& A = wkargs<R>();  // (A_arg is the same record, read where used)
   const uint32_t lid = lane_id();
   if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
     if (lid == 0)
@@ -587,9 +577,9 @@ struct DrainUnit {  // 64 B per slot
 static_assert(sizeof(DrainUnit) == 64, "DrainUnit layout");
 
 template <typename R, bool F32, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A_arg) {
+__global__ void __launch_bounds__(kTraceBlock) wf_drain([[maybe_unused]] WfArgs<R> A_arg) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  const WfArgs<R>& A = RTW_WF_KARG ? wkargs<R>() : A_arg;
+  const WfArgs<R>& A = wkargs<R>();  // (A_arg is the same record, read where used)
   __shared__ DrainUnit tab_all[kTraceBlock / 64][kSegCap];
   __shared__ uint32_t list_all[kTraceBlock / 64][64];
   const uint32_t lid = lane_id();
@@ -699,13 +689,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain(WfArgs<R> A_arg) {
       // lanes of one wave see each other's vector memory operations in order,
       // AMDGPU memory model), not a workgroup-scope one, whose release would
       // wait for every store of the wave to complete each iteration.
-#if RTW_RING_FENCE_WG
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
       wave_lds_sync();
-#endif
       // 4. Owners fold their ready samples in sample order (main.zig:393); a
       // unit done publishes its chunk sum and the slot takes the next unit.
       bool need_unit = false;

@@ -28,26 +28,12 @@
 #include "rtw_device.hpp"
 #include "rtw_libm.hpp"
 
-// BVH stack with its top entry held in a register (A/B switch; same traversal order).
-#ifndef RTW_WORLD_TOPCACHE
-#define RTW_WORLD_TOPCACHE 1
-#endif
-
-#ifndef RTW_RING_FENCE_WG
-#define RTW_RING_FENCE_WG 0  // (A/B: 1 = workgroup-scope fence around the tail ring)
-#endif
-
-#ifndef RTW_WORLD_DECIDE_REFS
-#define RTW_WORLD_DECIDE_REFS 1  // the node visit's decisions as refs made before its leaf tests
-                                 // (0: as bools; profiles/r04/world_decide_refs_ab.txt)
-#endif
-#ifndef RTW_WORLD_LANE_FLAGS
-#define RTW_WORLD_LANE_FLAGS 1  // the lane's state flags as bits of one word
-                                // (0: bools; profiles/r04/world_lane_flags_ab.txt)
-#endif
-#ifndef RTW_WORLD_TOUCH_NEXT
-#define RTW_WORLD_TOUCH_NEXT 1  // (A/B: 0 = off; profiles/r04/world_touch_next_ab.txt)
-#endif
+// (Measured choices that are now the only code: the BVH stack's top entry in a
+// register, profiles/r02/world_topcache_ab.txt; the node visit's decisions as
+// scalar refs made before its leaf tests, profiles/r04/world_decide_refs_ab.txt;
+// the lane's state flags as bits of one word, profiles/r04/world_lane_flags_ab.txt;
+// the left child's record line touched with every node visit,
+// profiles/r04/world_touch_next_ab.txt.)
 
 namespace rtwk {
 
@@ -335,9 +321,7 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   // votes below combine them with one compare's ballot in scalar ops.
   const uint64_t act = wballot(true), cull_ok = wballot(lc.ok);
   uint32_t sp = 0, node = 0;  // wave-uniform
-#if RTW_WORLD_TOPCACHE
   uint32_t top = 0;  // the stack's top entry (valid while sp > 0); stack[0 .. sp-1] hold the ones below it
-#endif
   auto leaf = [&](uint32_t ref) {
     WSTAMP(2)  // (MODE 2: node visits up to here)
     const uint32_t first = ref & 0x7FFFFFu, cnt = (ref >> 23) & kLeafCountMask;
@@ -381,18 +365,14 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     const RTW_CONST float* nd =
         reinterpret_cast<const RTW_CONST float*>(reinterpret_cast<const RTW_CONST char*>(cn) + (node << 6));
     static_assert(kNodeWords * 4 == 64, "node record size");
-#if RTW_WORLD_TOUCH_NEXT
     // The first word of record node + 1 — the left child whenever that child
     // is interior (depth-first layout, rtw_world_capi.hip Builder) — loaded
     // with this node's record (one wait covers both): the child's visit then
     // finds its line in the scalar cache.  (A padding record follows the last;
     // record node + 2 as well: 3 % slower, profiles/r04/world_touch_next_ab.txt.)
     const float touch = nd[kNodeWords];
-#endif
     const uint32_t r0 = __float_as_uint(nd[12]), r1 = __float_as_uint(nd[13]);
-#if RTW_WORLD_TOUCH_NEXT
     asm volatile("" ::"s"(touch), "s"(r0));  // (the touch's wait is the record's wait)
-#endif
     // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3
     const f2 x0 = pfma(f2{nd[0], nd[1]}, ix, oxl), x1 = pfma(f2{nd[6], nd[7]}, ix, oxh);
     const f2 y0 = pfma(f2{nd[2], nd[3]}, iy, oyl), y1 = pfma(f2{nd[8], nd[9]}, iy, oyh);
@@ -409,7 +389,6 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     // (the ballots are reused by the vote below: ballots of hit[] made again
     // there would first rebuild hit[] in VGPRs from these lane masks)
     const uint64_t b0 = wballot(hit[0]), b1 = wballot(hit[1]);
-#if RTW_WORLD_DECIDE_REFS
     // The visit's decisions as 32-bit refs (kNoRef: none) made before the leaf
     // tests (which do not change them), by scalar compares and selects in asm:
     // as C++ bools, LLVM kept them across the leaf calls as 64-bit lane masks
@@ -438,12 +417,8 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
     if (la != kNoRef) leaf(la);
     if (lb != kNoRef) leaf(lb);
     if (ps != kNoRef) {
-#if RTW_WORLD_TOPCACHE
       stack[sp++] = top;  // (entry 0 is a dummy when the stack was empty)
       top = ps;
-#else
-      stack[sp++] = ps;
-#endif
     }
     if (nx != kNoRef) {
       node = nx;
@@ -452,53 +427,9 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
         WSTAMP(2)
         break;
       }
-#if RTW_WORLD_TOPCACHE
       node = (uint32_t)__builtin_amdgcn_readfirstlane((int)top);
       top = stack[--sp];
-#else
-      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);
-#endif
     }
-#else
-    const bool any0 = b0 != 0, any1 = b1 != 0;
-    if (any0 && (r0 & kLeafBit)) leaf(r0);
-    if (any1 && (r1 & kLeafBit)) leaf(r1);
-    const bool i0 = any0 && !(r0 & kLeafBit), i1 = any1 && !(r1 & kLeafBit);
-    if (i0 && i1) {
-      // nearer child first by vote of the lanes that hit: lanes hitting child 0
-      // only or nearer-or-equal, and child 1 only or strictly nearer (masks
-      // combined in scalar ops, 32-bit popcounts).  (Ordering by the wave's
-      // majority ray sign along the split axis instead visits 101 nodes per
-      // segment against 84: 13 % slower, profiles/r03/world_signorder_ab.txt.)
-      const uint64_t le = wballot(tn[0] <= tn[1]), gt = wballot(tn[1] < tn[0]);
-      const uint32_t v0 = popc64(b0 & (~b1 | le)), v1 = popc64(b1 & (~b0 | gt));
-      const bool first0 = v0 >= v1;
-#if RTW_WORLD_TOPCACHE
-      stack[sp++] = top;  // (entry 0 is a dummy when the stack was empty)
-      top = first0 ? r1 : r0;
-#else
-      stack[sp++] = first0 ? r1 : r0;
-#endif
-      node = first0 ? r0 : r1;
-    } else if (i0) {
-      node = r0;
-    } else if (i1) {
-      node = r1;
-    } else {
-      if (sp == 0) {
-        WSTAMP(2)
-        break;
-      }
-#if RTW_WORLD_TOPCACHE
-      // The top entry lives in a register: the pop waits on no LDS read; the
-      // next top's LDS read is issued now and overlaps this node's loads.
-      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)top);
-      top = stack[--sp];
-#else
-      node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stack[--sp]);  // uniform: scalar loads
-#endif
-    }
-#endif
   }
 }
 
@@ -609,7 +540,6 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // the event that ends it (a miss adds T * background, a light T * emitted),
   // so that one term joins the chunk sum directly: sx + (0 + x) == sx + x
   // (x >= +0), the oracle's `rad` (rtw_world.c sample_b) without its registers.
-#if RTW_WORLD_LANE_FLAGS
   // The lane's state flags as bits of ONE word (a VGPR): as bools, each was a
   // 64-bit lane mask in SGPRs for the whole loop, and at the traversal's SGPR
   // peak the compiler spilled SGPRs to VGPR lanes (v_writelane / v_readlane,
@@ -620,11 +550,6 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   LaneFlag<4u> done{lane_flags};
   LaneFlag<8u> waiting{lane_flags};   // owner: its own samples done, waiting for the ones other lanes trace
   LaneFlag<16u> helping{lane_flags};  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
-#else
-  bool have_unit = false, have_ray = false, done = false;
-  bool waiting = false;  // owner: its own samples done, waiting for the ones other lanes trace
-  bool helping = false;  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
-#endif
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
   KStats st;  // MODE 2: phase stamps
@@ -899,13 +824,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     if constexpr (tail) {
       // the ring entries written above, read by other lanes of this wave
       // (wavefront scope: as wf_drain's ring, rtw_wavefront.hip)
-#if RTW_RING_FENCE_WG
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
       wave_lds_sync();
-#endif
       if (waiting) {
         uint32_t rdy = TL_READY[lid];
         const double* rb = WKA(ring) + (size_t)(blockIdx.x * kWorldBlock + threadIdx.x) * kTailWin * 3;

@@ -22,6 +22,7 @@
 // rtw_capi.hip helpers shared by both paths (same library).
 int rtw_fail(int status, const char* fmt, ...);
 int rtw_validate_params(const rtw_params* p);
+const char* rtw_dev_knob(const char* name);  // environment, -DRTW_MEASURE builds only
 size_t rtw_ws_total(const rtw_params* p);
 int rtw_device_cus(int dev);
 void rtw_fill_trace_args(rtwk::TraceArgs<double>& a, const rtw_camera* cam, const rtw_params* p, unsigned char* ws);
@@ -308,7 +309,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
-    if (getenv("RTW_BVH_DEBUG")) {  // root's two children: leaf (prims) or node, and their boxes
+    if (flags & RTW_WORLD_DEBUG_BVH) {  // root's two children: leaf (prims) or node, and their boxes
       for (int c = 0; c < 2; ++c) {
         uint32_t ref;
         std::memcpy(&ref, bvh.nodes.data() + 12 + c, 4);
@@ -383,7 +384,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     }
     cull_cmax = std::nextafter((float)(cmax_c + cmax_d), INFINITY);
     cull_rho = std::nextafter((float)rho_max, INFINITY);
-    const char* nc = getenv("RTW_WORLD_NOCULL");  // development knob (A/B): no leaf pretest
+    const char* nc = rtw_dev_knob("RTW_WORLD_NOCULL");  // development knob (A/B): no leaf pretest
     if (!leaf_refs.empty() && cull_cmax <= rtwc::kCmaxLimit && !(nc && *nc)) {
       cull.assign((size_t)16 * n, 0.0f);
       for (uint32_t slot : leaf_refs) {
@@ -576,13 +577,12 @@ struct WorldLaunchCfg {
 WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   WorldLaunchCfg c;
   c.lds = rtwk::world_lds_bytes(w->view.n_perlins);
-  // Register-allocation target (RTW_WORLD_OCC development knob overrides).
-  const char* oc = getenv("RTW_WORLD_OCC");
-  const int occ = (oc && *oc) ? atoi(oc) : world_occ_default(w);
-  // Kernel instantiation for the world's features (RTW_WORLD_FEAT=all: the
-  // general kernel, development knob for A/B; every set gives the same bits).
-  const char* fe = getenv("RTW_WORLD_FEAT");
-  c.fs = rtwk::world_feature_set((fe && !std::strcmp(fe, "all")) ? 15u : w->feat);
+  // Register-allocation target in waves per SIMD (params.world_waves, 0 = the
+  // feature set's default).
+  const int occ = p->world_waves ? (int)p->world_waves : world_occ_default(w);
+  // Kernel instantiation for the world's features (params.world_features
+  // RTW_WORLD_FEATURES_ALL: the general kernel; every set gives the same bits).
+  c.fs = rtwk::world_feature_set(p->world_features == RTW_WORLD_FEATURES_ALL ? 15u : w->feat);
   c.oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
   static std::mutex mu;
   static int bpc_cache[16][5] = {};
@@ -603,7 +603,8 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
 }
 
 int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
-                 uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode) {
+                 uint8_t* d_rgb, float* d_mean, hipStream_t stream, rtw_timer timer, int mode,
+                 uint32_t* tail_ran = nullptr) {
   if (!w || !cam) return rtw_fail(RTW_EINVAL, "world/camera is NULL");
   const int v = rtw_validate_params(p);
   if (v != RTW_OK) return v;
@@ -627,12 +628,14 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   a.margin = bvh_margin(w, cam);
   a.counts = reinterpret_cast<unsigned long long*>(wsb + rtw_ws_stats_off(p));
   const WorldLaunchCfg c = world_cfg(w, p, dev);
-  // Tail dealing (default; RTW_WORLD_TAIL=0: off) needs the rings in the
-  // workspace (rtw_world_workspace_bytes); a workspace of only
-  // rtw_workspace_bytes(params) renders without it — the same image.
-  const char* te = getenv("RTW_WORLD_TAIL");
+  // Tail dealing (default; development knob RTW_WORLD_TAIL=0: off) needs the
+  // rings in the workspace (rtw_world_workspace_bytes); a workspace of only
+  // rtw_workspace_bytes(params) renders without it — the same image, and
+  // rtw_world_render_counts_ex reports which ran.
+  const char* te = rtw_dev_knob("RTW_WORLD_TAIL");
   a.tail_deal = ((te && *te == '0') || ws_bytes < c.ring_off + c.ring_bytes) ? 0u : 1u;
   a.ring = a.tail_deal ? reinterpret_cast<double*>(wsb + c.ring_off) : nullptr;
+  if (tail_ran) *tail_ran = a.tail_deal;
   const size_t lds = c.lds;
   const uint32_t grid = c.grid;
   const int oi = c.oi, fs = c.fs;
@@ -665,13 +668,13 @@ int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params
   return world_launch(w, cam, p, ws, ws_bytes, d_rgb, d_mean, static_cast<hipStream_t>(stream), timer, 0);
 }
 
-int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
-                            uint64_t counts_out[4]) {
+int rtw_world_render_counts_ex(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
+                               uint64_t counts_out[6]) {
   if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
 #ifdef RTW_MEASURE
   // RTW_WORLD_PHASE=1 (diagnostic build): a phase-stamp pass first; its wave-cycle
   // shares go to stderr (tools/world_bench.py --phase).
-  const char* ph = getenv("RTW_WORLD_PHASE");
+  const char* ph = rtw_dev_knob("RTW_WORLD_PHASE");
   if (ph && *ph == '1') {
     int st2 = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 2);
     if (st2 != RTW_OK) return st2;
@@ -686,18 +689,27 @@ int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params
     for (int i = 0; i < 5; ++i) fprintf(stderr, "[world phase] %-22s %6.2f %%\n", nm[i], 100.0 * (double)q[i] / tot);
   }
 #endif
-  const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1);
+  uint32_t tail = 0;
+  const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1, &tail);
   if (st != RTW_OK) return st;
   if (hipDeviceSynchronize() != hipSuccess) return rtw_fail(RTW_EHIP, "world counts pass failed");
   unsigned long long c[5];
   if (hipMemcpy(c, static_cast<unsigned char*>(ws) + rtw_ws_stats_off(p), sizeof(c), hipMemcpyDeviceToHost) !=
       hipSuccess)
     return rtw_fail(RTW_EHIP, "counts copy failed");
-  for (int i = 0; i < 4; ++i) counts_out[i] = c[i];
-  if (const char* v = getenv("RTW_COUNTS_VERBOSE"); v && *v == '1')  // diagnostic: lanes busy per wave iteration
-    fprintf(stderr, "[world counts] wave iterations %llu, segments per wave iteration %.2f of 64\n", c[4],
-            (double)c[1] / (double)(c[4] ? c[4] : 1));
+  for (int i = 0; i < 5; ++i) counts_out[i] = c[i];  // samples, segments, node visits, primitive tests, wave iterations
+  counts_out[5] = tail;
   return RTW_OK;
+}
+
+int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
+                            uint64_t counts_out[4]) {
+  if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
+  uint64_t c[6];
+  const int st = rtw_world_render_counts_ex(w, cam, p, ws, ws_bytes, c);
+  if (st == RTW_OK)
+    for (int i = 0; i < 4; ++i) counts_out[i] = c[i];
+  return st;
 }
 
 int rtw_world_render(const rtw_camera* cam, const rtw_world_desc* desc, const rtw_params* p, uint8_t* rgb_out,

@@ -29,7 +29,14 @@ LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 PRECISION = {"f64": 0, "f32": 1}
 ENGINE = {"megakernel": 0, "wavefront": 1}
 DEFAULT_WF_PATHS = 3 << 18  # rtw_hip.h RTW_DEFAULT_WF_PATHS
-DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (env RTW_WF_SETS overrides)
+DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (params.wf_sets overrides)
+WF_DRAIN = {"samples": 0, "slots": 1, "none": 2}  # rtw_wf_drain
+WF_FORM = {"fused": 0, "split": 1}  # rtw_wf_form
+WORLD_FEATURES = {"auto": 0, "all": 1}  # rtw_world_features
+STATS_WORDS = 16  # rtw_hip.h RTW_STATS_WORDS
+STAT_NAMES = ["samples", "segments", "f32_skips", "cand_wave_iters", "cand_lanes", "disc_ge0_lanes",
+              "sphere_loop_wave_iters", "cull_survivor_lanes", "cull_exact_wave_iters", "drain_segments",
+              "drain_samples", "cluster_wave_tests", "cluster_wave_skips", "drain_wave_iters"]  # RTW_STAT_*
 DEFAULT_CHUNK = 32
 COVER_BACKGROUND = (0.70, 0.80, 1.00)
 
@@ -61,7 +68,9 @@ class Params(C.Structure):
                 ("max_depth", C.c_uint32), ("seed", C.c_uint64), ("background", C.c_double * 3),
                 ("row_begin", C.c_uint32), ("row_stride", C.c_uint32), ("row_count", C.c_uint32),
                 ("chunk", C.c_uint32), ("precision", C.c_uint32), ("device", C.c_int32),
-                ("engine", C.c_uint32), ("wf_paths", C.c_uint32)]
+                ("engine", C.c_uint32), ("wf_paths", C.c_uint32),
+                ("wf_sets", C.c_uint32), ("wf_drain", C.c_uint32), ("wf_form", C.c_uint32),
+                ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 _lib = None
@@ -110,6 +119,8 @@ def lib() -> C.CDLL:
                                     C.c_uint64 * 4]
     L.rtw_render_counts_ex.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                        C.c_uint64 * 6]
+    L.rtw_render_stats.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
+                                   C.c_uint64 * STATS_WORDS]
     _lib = L
     return L
 
@@ -165,13 +176,20 @@ def cover_scene(seed: int = 42):
 
 def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACKGROUND, row_begin=0,
                 row_stride=1, row_count=None, chunk=0, precision="f64", device=-1, engine="megakernel",
-                wf_paths=0) -> Params:
+                wf_paths=0, wf_sets=0, wf_drain="samples", wf_form="fused", world_waves=0,
+                world_features="auto") -> Params:
+    """rtw_params (ABI v4): every engine choice is a field (0 / the first
+    name = the library default); nothing is read from the environment."""
     if row_count is None:
         row_count = (height - row_begin + row_stride - 1) // row_stride
     prec = PRECISION[precision] if isinstance(precision, str) else int(precision)
     eng = ENGINE[engine] if isinstance(engine, str) else int(engine)
+
+    def enum(v, names):
+        return names[v] if isinstance(v, str) else int(v)
     return Params(width, height, spp, max_depth, seed, (C.c_double * 3)(*background), row_begin, row_stride,
-                  row_count, chunk, prec, device, eng, wf_paths)
+                  row_count, chunk, prec, device, eng, wf_paths, wf_sets, enum(wf_drain, WF_DRAIN),
+                  enum(wf_form, WF_FORM), world_waves, enum(world_features, WORLD_FEATURES), 0)
 
 
 def _arr(x, typ):
@@ -263,6 +281,13 @@ class DeviceScene:
                                           workspace_bytes_, out))
         return {"samples": int(out[0]), "segments": int(out[1]), "static_tests": int(out[2]),
                 "moving_tests": int(out[3]), "drain_segments": int(out[4]), "drain_samples": int(out[5])}
+
+    def stats(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int) -> dict:
+        """The counting pass's raw statistics words (rtw_render_stats, RTW_STAT_*)."""
+        out = (C.c_uint64 * STATS_WORDS)()
+        _check(lib().rtw_render_stats(self.h, C.byref(cam), C.byref(params), C.c_void_p(workspace_ptr),
+                                      workspace_bytes_, out))
+        return {n: int(out[i]) for i, n in enumerate(STAT_NAMES)}
 
     def close(self):
         if self.h:

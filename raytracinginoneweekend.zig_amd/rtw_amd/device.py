@@ -48,3 +48,8 @@ class TorchRenderer:
         ptr, nbytes = self._ws_ptr(params)
         torch.cuda.synchronize(self.device)
         return self.scene.counts(cam, params, ptr, nbytes)
+
+    def stats(self, cam: Camera, params: Params) -> dict:
+        ptr, nbytes = self._ws_ptr(params)
+        torch.cuda.synchronize(self.device)
+        return self.scene.stats(cam, params, ptr, nbytes)

@@ -26,6 +26,7 @@ XF_TRANSLATE, XF_ROTATE_Y = 0, 1
 TEX_SOLID, TEX_CHECKER, TEX_NOISE, TEX_IMAGE = 0, 1, 2, 3
 WMAT_LAMBERT, WMAT_METAL, WMAT_DIELECTRIC, WMAT_LIGHT = 0, 1, 2, 3
 WORLD_LINEAR = 1
+WORLD_DEBUG_BVH = 2  # rtw_hip.h RTW_WORLD_DEBUG_BVH: the BVH root's children to stderr (diagnostic)
 SCENES = {1: "cover", 2: "two_spheres", 3: "two_perlin_spheres", 4: "earth", 5: "simple_light",
           6: "cornell_box", 7: "globe_10k"}
 
@@ -91,6 +92,8 @@ def _wlib():
     L.rtw_world_render.argtypes = [P(Camera), P(WorldDesc), P(Params), C.c_void_p, C.c_void_p]
     L.rtw_world_render_counts.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                           C.c_uint64 * 4]
+    L.rtw_world_render_counts_ex.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
+                                             C.c_uint64 * 6]
     L._world_ready = True
     return L
 
@@ -270,9 +273,10 @@ def render_world(cam: Camera, desc: WorldDesc, params: Params, want_mean=False):
 class DeviceWorld:
     """A world resident in HBM of the current device (rtw_world_create)."""
 
-    def __init__(self, desc: WorldDesc, linear: bool = False):
+    def __init__(self, desc: WorldDesc, linear: bool = False, debug_bvh: bool = False):
         self.h = C.c_void_p()
-        _check(_wlib().rtw_world_create(C.byref(desc), WORLD_LINEAR if linear else 0, C.byref(self.h)))
+        flags = (WORLD_LINEAR if linear else 0) | (WORLD_DEBUG_BVH if debug_bvh else 0)
+        _check(_wlib().rtw_world_create(C.byref(desc), flags, C.byref(self.h)))
 
     def bvh_info(self) -> dict:
         info = (C.c_uint32 * 4)()
@@ -296,11 +300,13 @@ class DeviceWorld:
                                                timer.h if timer is not None else None))
 
     def counts(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int) -> dict:
-        out = (C.c_uint64 * 4)()
-        _check(_wlib().rtw_world_render_counts(self.h, C.byref(cam), C.byref(params), C.c_void_p(workspace_ptr),
-                                               workspace_bytes_, out))
+        """rtw_world_render_counts_ex: the counts, the persistent kernel's wave
+        iterations and whether tail dealing ran (the workspace held the rings)."""
+        out = (C.c_uint64 * 6)()
+        _check(_wlib().rtw_world_render_counts_ex(self.h, C.byref(cam), C.byref(params),
+                                                  C.c_void_p(workspace_ptr), workspace_bytes_, out))
         return {"samples": int(out[0]), "segments": int(out[1]), "node_visits": int(out[2]),
-                "prim_tests": int(out[3])}
+                "prim_tests": int(out[3]), "wave_iters": int(out[4]), "tail_dealing": bool(out[5])}
 
     def close(self):
         if self.h:

@@ -54,13 +54,17 @@ def main():
     kat["defaultprng42_u64_after_lz12_float"] = r.next()
     r = O.ZigRandom(7)
     kat["defaultprng7_f32_hex"] = [float.hex(r.f32()) for _ in range(8)]
-    # Tier-B counter-based stream: SplitMix64 blocks of (seed 42, pixel, sample)
+    # Tier-B counter-based stream: Weyl blocks of (seed 42, pixel, sample),
+    # draws = ro_tb_mix of the states (round 5; C == the Python tb_mix)
     import ctypes as C
     L = O.lib()
     kat["tierb_state_42_p0_s0"] = L.ro_tierb_state(42, 0, 0)
     kat["tierb_state_42_p1234_s77"] = L.ro_tierb_state(42, 1234, 77)
     st = C.c_uint64(L.ro_tierb_state(42, 1234, 77))
     kat["tierb_42_p1234_s77_f64_hex"] = [float.hex(L.ro_sm_f64(C.byref(st))) for _ in range(6)]
+    kat["tb_mix_in"] = [0, 1, 1 << 32, 0x9E3779B97F4A7C15, (1 << 64) - 1, kat["tierb_state_42_p1234_s77"]]
+    kat["tb_mix_out"] = [L.ro_tb_mix(x) for x in kat["tb_mix_in"]]
+    assert kat["tb_mix_out"] == [P.tb_mix(x) for x in kat["tb_mix_in"]], "C and Python tb_mix disagree"
     with open(os.path.join(HERE, "rng_kat.json"), "w") as f:
         json.dump(kat, f, indent=1)
 

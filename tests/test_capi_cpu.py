@@ -7,7 +7,7 @@ import os
 
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, REPO
 from helpers import to_oracle_camera
 
 
@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol(rtw):
 
 
 def test_abi_version(rtw):
-    assert rtw.abi_version() == 3
+    assert rtw.abi_version() == 4
 
 
 def test_struct_layouts_match_header(rtw):
@@ -27,7 +27,7 @@ def test_struct_layouts_match_header(rtw):
     assert C.sizeof(rtw.Material) == 8 + 3 * 8 * 2 + 16
     assert C.sizeof(rtw.Sphere) == 6 * 8 + 3 * 8 + 8
     assert C.sizeof(rtw.Camera) == 7 * 24 + 24
-    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12 + 8
+    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12 + 8 + 6 * 4  # + ABI v4 engine fields
 
 
 def test_cover_scene_equals_oracle_golden(rtw):
@@ -114,17 +114,16 @@ def test_workspace_bytes(rtw):
 def test_workspace_bytes_wavefront(rtw, monkeypatch, sets, ring):
     """Wavefront engine: + two SoA path queues (each with the fused engine's
     hit root / winner per path), the split engine's hit arrays, the home
-    slots and (wf_drain only: RTW_WF_DRAIN != 0) its ring of 32 R x3 sample
+    slots and (wf_drain only: params.wf_drain RTW_WF_DRAIN_SAMPLES) its ring of 32 R x3 sample
     radiances (rtw_capi.hip ws_layout) per in-flight path, + per-segment
-    words; wf_paths is split over RTW_WF_SETS queue sets, so the bytes per
+    words; wf_paths is split over params.wf_sets queue sets, so the bytes per
     path do not grow with the sets (exact bounds: an upper bound per path,
     ADVICE r3)."""
-    monkeypatch.setenv("RTW_WF_SETS", str(sets))
-    monkeypatch.setenv("RTW_WF_DRAIN", "1" if ring else "0")
     base = rtw.workspace_bytes(rtw.make_params(1200, 675, 500))
     for prec, r in (("f64", 8), ("f32", 4)):
         for n in (1 << 16, 1 << 20, 3 << 18):
-            p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n)
+            p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n, wf_sets=sets,
+                                wf_drain="samples" if ring else "slots")
             per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + 32 + (32 * 3 * r if ring else 0)
             segs = -(-n // (64 * sets))  # per set: one 64-path queue segment = 2 counts + a unit reservoir
             paths = segs * 64
@@ -134,6 +133,69 @@ def test_workspace_bytes_wavefront(rtw, monkeypatch, sets, ring):
             assert extra <= n * (per_path + 1) + sets * (64 * per_path + 64 * 256)  # per-path upper bound
     d = rtw.make_params(64, 36, 1, engine="wavefront")
     assert rtw.workspace_bytes(d) > rtw.DEFAULT_WF_PATHS * 100
+
+
+ENV_KNOBS = {  # every environment variable a development (-DRTW_MEASURE) build reads
+    "RTW_WF_SETS": "1", "RTW_WF_DRAIN": "0", "RTW_WF_FINISH": "0", "RTW_WF_FUSED": "0", "RTW_WF_BATCH": "8",
+    "RTW_WF_GRID": "2", "RTW_WF_SET_GRID": "2", "RTW_WF_TIMEOUT_S": "1", "RTW_UNIT_ORDER": "rev",
+    "RTW_VARIANT": "516", "RTW_WORLD_OCC": "1", "RTW_WORLD_FEAT": "all", "RTW_WORLD_TAIL": "0",
+    "RTW_PHASE_PROFILE": "1", "RTW_COUNTS_VERBOSE": "1"}
+
+
+def test_workspace_bytes_ignore_the_environment(rtw):
+    """ABI v4: the product library reads no environment
+    variable on the render path, so rtw_workspace_bytes is a function of the
+    params alone — checked in a fresh process with every knob set."""
+    import json
+    import subprocess
+    import sys
+    code = (
+        "import json, sys; sys.path.insert(0, %r); import rtw_amd as R\n"
+        "out = []\n"
+        "for eng in ('megakernel', 'wavefront'):\n"
+        "    for prec in ('f64', 'f32'):\n"
+        "        for kw in ({}, {'wf_sets': 1}, {'wf_sets': 3, 'wf_drain': 'slots'}, {'wf_drain': 'none'}):\n"
+        "            p = R.make_params(1200, 675, 500, precision=prec, engine=eng, **kw)\n"
+        "            out.append(R.workspace_bytes(p))\n"
+        "print(json.dumps(out))\n") % os.path.join(REPO, "raytracinginoneweekend.zig_amd")
+    env0 = {k: v for k, v in os.environ.items() if not k.startswith("RTW_")}
+    a = json.loads(subprocess.run([sys.executable, "-c", code], env=env0, capture_output=True, text=True,
+                                  check=True).stdout)
+    b = json.loads(subprocess.run([sys.executable, "-c", code], env={**env0, **ENV_KNOBS}, capture_output=True,
+                                  text=True, check=True).stdout)
+    assert a == b
+    # and the params fields do change it (wavefront f64: without the drain ring
+    # for wf_finish / no drain; the megakernel ignores the wavefront fields)
+    assert a[8] != a[10] and a[8] != a[11] and len(set(a[0:4])) == 1
+
+
+def test_product_library_reads_no_environment():
+    """The only getenv of the product sources is the development-knob helper,
+    compiled in the -DRTW_MEASURE build alone."""
+    import glob
+    import re
+    src = os.path.join(REPO, "raytracinginoneweekend.zig_amd", "csrc")
+    hits = []
+    for f in glob.glob(os.path.join(src, "*.hip")) + glob.glob(os.path.join(src, "*.cpp")) + \
+            glob.glob(os.path.join(src, "*.hpp")):
+        for i, line in enumerate(open(f), 1):
+            if re.search(r"\bgetenv\s*\(", line):
+                hits.append((os.path.basename(f), i, line.strip()))
+    assert [h[:2] for h in hits] == [("rtw_capi.hip", hits[0][1])], hits
+    txt = open(os.path.join(src, "rtw_capi.hip")).read()
+    i = txt.find("const char* dev_knob(const char* name) {")
+    body = txt[i:txt.find("}", txt.find("#endif", i))]
+    assert "#ifdef RTW_MEASURE" in body and "return getenv(name);" in body and "return nullptr;" in body
+
+
+@pytest.mark.parametrize("field,value", [("wf_sets", 5), ("wf_drain", 3), ("wf_form", 2), ("world_waves", 5),
+                                         ("world_features", 2), ("reserved", 1)])
+def test_params_v4_fields_validated(rtw, field, value):
+    p = rtw.make_params(64, 36, 1, engine="wavefront")
+    setattr(p, field, value)
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.workspace_bytes(p)
+    assert e.value.status == rtw.RTW_EINVAL
 
 
 def test_no_cpu_fallback_without_gpu(rtw):

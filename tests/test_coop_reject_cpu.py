@@ -4,7 +4,7 @@ mix of requests — unit-ball points (dim 3, rand.zig:22-28), lens-disk points
 plus the following time draw (dim 2, rand.zig:30-36 + main.zig:99) and one
 speculative dielectric draw (dim 1) — every lane gets exactly the point, the
 final RNG state and the extra draw of its own sequential loop under the
-Tier-B counter RNG (each draw one SplitMix64 Weyl step; rare long-leading-zero
+Tier-B counter RNG (each draw one Weyl step through the Tier-B mixer; rare long-leading-zero
 words from the draw's extension stream).  Pure Python, test infrastructure."""
 import math
 import random
@@ -17,10 +17,18 @@ GAMMA = 0x9E3779B97F4A7C15
 EXT = 0x5851F42D4C957F2D
 
 
-def mix(z):
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
-    return z ^ (z >> 31)
+def mix(z):  # Tier-B mixer (oracle/rtw_oracle.c ro_tb_mix): four Feistel half-rounds
+    hi, lo = z >> 32, z & 0xFFFFFFFF
+    for i, m in enumerate((0xD2511F53, 0xCD9E8D57, 0x9E3779B1, 0x85EBCA6B)):
+        if i % 2 == 0:
+            t = hi * m
+            lo ^= t >> 32
+            hi = t & 0xFFFFFFFF
+        else:
+            t = lo * m
+            hi ^= t >> 32
+            lo = t & 0xFFFFFFFF
+    return (hi << 32) | lo
 
 
 def clz64(v):

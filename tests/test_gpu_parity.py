@@ -194,15 +194,11 @@ def test_clustered_pretest_mixed_time_groups(rtw, oracle, capfd, monkeypatch):
     o = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam), **kw)
     assert_parity(g, o, "clustered, 3 time groups")
     assert g.std() > 5
-    monkeypatch.setenv("RTW_COUNTS_VERBOSE", "1")
     R = TorchRenderer(sph, mats, 0)
-    R.counts(cam, rtw.make_params(192, 108, 12, chunk=5))
-    err = capfd.readouterr().err
-    line = [ln for ln in err.splitlines() if "cluster_wave_skips" in ln][-1]
-    f = line.split()
-    tests, skips = int(f[f.index("cluster_wave_tests") + 1]), int(f[f.index("cluster_wave_skips") + 1])
-    print(line)
-    assert tests > 0 and skips > 0, line
+    st = R.stats(cam, rtw.make_params(192, 108, 12, chunk=5))  # rtw_render_stats (RTW_STAT_*)
+    tests, skips = st["cluster_wave_tests"], st["cluster_wave_skips"]
+    print(st)
+    assert tests > 0 and skips > 0, st
     # a shutter outside one group turns the clusters off (flat pretest): same image as the oracle too
     cam2 = rtw.camera_init((13, 2, 3), (0, 0.3, 0), (0, 1, 0), 30.0, ASPECT, 0.1, 10.0, 0.0, 1.2)
     g2 = gpu_render(rtw, cam2, sph, mats, **kw)

@@ -20,33 +20,44 @@ from test_gpu_parity import ASPECT, assert_parity, custom_scene, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["samples", "finish", "queues"])
-def drain(request, monkeypatch):
-    """Every test runs with the three drains: in registers once slots retire,
-    by wf_drain (samples dealt to free lanes, the default) or wf_finish
-    (RTW_WF_DRAIN=0), and the bounce kernels' queues to the end
-    (RTW_WF_FINISH=0); read by the library on every render."""
-    monkeypatch.setenv("RTW_WF_FINISH", "0" if request.param == "queues" else "1")
-    monkeypatch.setenv("RTW_WF_DRAIN", "0" if request.param == "finish" else "1")
+@pytest.fixture(params=["samples", "finish", "queues"])
+def drain(request):
+    """Every test runs with the three drains (params.wf_drain): in registers
+    once slots retire, by wf_drain (samples dealt to free lanes, the default)
+    or wf_finish (RTW_WF_DRAIN_SLOTS), and the bounce kernels' queues to the
+    end (RTW_WF_DRAIN_NONE)."""
     return request.param
 
 
-@pytest.fixture(autouse=True, params=["fused", "split"])
-def engine_form(request, monkeypatch):
-    """... and both forms of the engine: one fused kernel per bounce (shade +
-    the next closest hit, the default) and separate extend / shade kernels
-    (RTW_WF_FUSED=0)."""
-    monkeypatch.setenv("RTW_WF_FUSED", "1" if request.param == "fused" else "0")
+@pytest.fixture(params=["fused", "split"])
+def engine_form(request):
+    """... and both forms of the engine (params.wf_form): one fused kernel per
+    bounce (shade + the next closest hit, the default) and separate extend /
+    shade kernels."""
     return request.param
 
 
-@pytest.fixture(autouse=True, params=["sets1", "sets2"])
-def queue_sets(request, monkeypatch):
-    """... and one or two queue sets (RTW_WF_SETS): the in-flight paths split
-    over independent sets on their own HIP streams, sharing the device unit
-    queue (a unit still belongs to one slot, so the bits cannot change)."""
-    monkeypatch.setenv("RTW_WF_SETS", request.param[-1])
+@pytest.fixture(params=["sets1", "sets2"])
+def queue_sets(request):
+    """... and one or two queue sets (params.wf_sets): the in-flight paths
+    split over independent sets on their own HIP streams, sharing the device
+    unit queue (a unit still belongs to one slot, so the bits cannot change)."""
     return int(request.param[-1])
+
+
+@pytest.fixture(autouse=True)
+def wf_config(rtw, monkeypatch, drain, engine_form, queue_sets):
+    """The engine configuration travels in rtw_params (ABI v4): every params
+    the test makes carries this case's wf_drain / wf_form / wf_sets."""
+    orig = rtw.make_params
+    cfg = dict(wf_drain={"samples": "samples", "finish": "slots", "queues": "none"}[drain], wf_form=engine_form,
+               wf_sets=queue_sets)
+
+    def make_params(*a, **kw):
+        for k, v in cfg.items():
+            kw.setdefault(k, v)
+        return orig(*a, **kw)
+    monkeypatch.setattr(rtw, "make_params", make_params)
 
 
 @pytest.fixture(scope="module")

@@ -189,13 +189,12 @@ def test_world_register_budgets_agree(rtw, W, earth, scene, w, spp, monkeypatch)
     cam = b.camera()
     h = rtw.image_height(w, b.settings.aspect)
     p = params(rtw, b, w, h, spp)
-    # and per feature set (RTW_WORLD_FEAT=all: the general kernel instead of
-    # the one compiled for this world's features)
+    # and per feature set (params.world_features "all": the general kernel
+    # instead of the one compiled for this world's features)
     outs = []
-    for occ in ("1", "3", "4"):
-        for feat in ("", "all"):
-            monkeypatch.setenv("RTW_WORLD_OCC", occ)
-            monkeypatch.setenv("RTW_WORLD_FEAT", feat)
+    for occ in (1, 3, 4):
+        for feat in (0, 1):
+            p.world_waves, p.world_features = occ, feat
             rgb, mean, _, _ = _render_dev(rtw, W, b, cam, p, linear=False)
             outs.append((rgb, mean))
     for rgb, mean in outs[1:]:

@@ -106,7 +106,8 @@ def test_sqrt_threshold_equivalence():
 
 
 def test_tierb_counter_stream(oracle, kat):
-    """Tier-B RNG: SplitMix64 state base + (((p << 24) | s) << 16) * gamma."""
+    """Tier-B RNG: Weyl state base + (((p << 24) | s) << 16) * gamma, draws
+    ro_tb_mix of the following states (oracle/rtw_oracle.c)."""
     import ctypes as C
     L = oracle.lib()
     gamma = 0x9E3779B97F4A7C15
@@ -117,9 +118,45 @@ def test_tierb_counter_stream(oracle, kat):
     assert L.ro_tierb_state(42, 1234, 77) == kat["tierb_state_42_p1234_s77"]
     st = C.c_uint64(L.ro_tierb_state(42, 1234, 77))
     assert [float.hex(L.ro_sm_f64(C.byref(st))) for _ in range(6)] == kat["tierb_42_p1234_s77_f64_hex"]
-    # the stream IS SplitMix64.init(state).next(): check against the Python restatement
+    assert [L.ro_tb_mix(x) for x in kat["tb_mix_in"]] == kat["tb_mix_out"]
+    # the draws ARE tb_mix of the Weyl states: check against the independent
+    # Python restatement, through Random.float's exponent / mantissa split
     import rtw_oracle_py as P
-    g = P.SplitMix64(L.ro_tierb_state(42, 1234, 77))
-    st = C.c_uint64(L.ro_tierb_state(42, 1234, 77))
+    w = L.ro_tierb_state(42, 1234, 77)
+    st = C.c_uint64(w)
     for _ in range(100):
-        assert L.ro_splitmix64_next(C.byref(st)) == g.next()
+        w = (w + gamma) % (1 << 64)
+        v = P.tb_mix(w)
+        assert L.ro_tb_mix(w) == v
+        x = L.ro_sm_f64(C.byref(st))
+        assert st.value == w
+        lz = 64 - v.bit_length()
+        if lz < 12:
+            assert x == math.ldexp(1.0 + (v & ((1 << 52) - 1)) / 2.0 ** 52, -1 - lz)
+
+
+def test_tb_mix_is_a_bijection_on_samples():
+    """Four Feistel half-rounds: invertible, so distinct Weyl states give
+    distinct draws (inverse restated here, applied to random words)."""
+    import random
+    import rtw_oracle_py as P
+    ms = (0xD2511F53, 0xCD9E8D57, 0x9E3779B1, 0x85EBCA6B)
+    inv = [pow(m, -1, 1 << 32) for m in ms]
+
+    def unmix(z):
+        hi, lo = z >> 32, z & 0xFFFFFFFF
+        for i in (3, 2, 1, 0):
+            if i % 2 == 0:  # forward: t = hi*m; lo ^= t>>32; hi = lo32(t)
+                h0 = (hi * inv[i]) & 0xFFFFFFFF
+                lo ^= (h0 * ms[i]) >> 32
+                hi = h0
+            else:
+                l0 = (lo * inv[i]) & 0xFFFFFFFF
+                hi ^= (l0 * ms[i]) >> 32
+                lo = l0
+        return (hi << 32) | lo
+
+    rnd = random.Random(5)
+    for _ in range(2000):
+        z = rnd.getrandbits(64)
+        assert unmix(P.tb_mix(z)) == z

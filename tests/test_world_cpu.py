@@ -274,18 +274,20 @@ def test_world_oracle_scene1_equals_cover_oracle(oracle):
 @pytest.mark.parametrize("scene", [5, 6])
 def test_tier_c_emissive_forward_vs_recursive(oracle, scene):
     """Tier B evaluates rayColor forward (rad += T * emitted); Tier A is the
-    reference's recursion.  Same scene, same spp: image means agree within
-    the seed noise (sum over ~4k pixels)."""
+    reference's recursion.  Same scene, same spp: Tier A's image mean lies
+    within the seed-to-seed spread of Tier B's (8 seeds; z <= 4 against the
+    spread, which is ~0.45 LSB for scene 5's dim, light-lit image at 24 spp —
+    one seed pair is too noisy an estimate of it)."""
     w = oracle.OracleWorld(scene, 42)
     W_, H_ = (48, 32) if scene == 5 else (40, 40)
     cam = w.camera()
     spp = 24
     a, _ = w.render_tier_a(cam, W_, H_, spp)
-    b, _ = w.render_tier_b(cam, W_, H_, spp)
-    b2, _ = w.render_tier_b(cam, W_, H_, spp, seed=777)
-    da = np.abs(a.astype(float).mean((0, 1)) - b.astype(float).mean((0, 1))).max()
-    dn = np.abs(b2.astype(float).mean((0, 1)) - b.astype(float).mean((0, 1))).max()
-    assert da <= max(3 * dn, 1.0), (da, dn)
+    mb = np.array([w.render_tier_b(cam, W_, H_, spp, seed=sd)[0].astype(float).mean((0, 1))
+                   for sd in (42, 777, 1, 2, 3, 4, 5, 6)])
+    sd_b = mb.std(0, ddof=1)
+    z = np.abs(a.astype(float).mean((0, 1)) - mb.mean(0)) / (sd_b * np.sqrt(1 + 1 / len(mb)))
+    assert z.max() <= 4.0, (z, mb.mean(0), sd_b)
 
 
 def test_cornell_oracle_geometry(oracle):
@@ -319,9 +321,8 @@ def test_globe_bvh_isolates_the_ground_at_the_root():
     code = ("import sys; sys.path.insert(0, %r)\n"
             "from rtw_amd import world as W\n"
             "b = W.BuiltScene(7, 42, image=W.earth_map())\n"
-            "try:\n    W.DeviceWorld(b.desc).close()\nexcept Exception:\n    pass\n") % os.path.join(REPO, "raytracinginoneweekend.zig_amd")
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, RTW_BVH_DEBUG="1"))
+            "try:\n    W.DeviceWorld(b.desc, debug_bvh=True).close()\nexcept Exception:\n    pass\n") % os.path.join(REPO, "raytracinginoneweekend.zig_amd")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     lines = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh] root child")]
     assert len(lines) == 2, p.stderr
     assert "leaf of 1, box x [-1000, 1000] y [-2000, 0] z [-1000, 1000]" in lines[0]
