@@ -78,7 +78,7 @@ def parse():
     return parse_args()
 
 
-EVIDENCE_ROUNDS = ("r04", "r03", "r02", "r01")  # newest first
+EVIDENCE_ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # newest first
 
 
 def evidence(name):
@@ -291,14 +291,28 @@ def world_roofline(scene, s, kernel_ms, info):
 class ClockWindow:
     """The average shader clock over a timed loop (box-to-box
     spreads read beside the clock): rtw_sclk_probe on a side stream, one wave
-    spinning for ~90 % of the loop's expected wall time (est_ms), read after."""
+    spinning for ~90 % of the loop's expected wall time (est_ms, from the LAST
+    warm-up step: the first ones carry code-object loads and allocations),
+    read after.  window_ms goes into the line beside the loop's wall time."""
 
     def __init__(self, R, torch, est_ms):
         self.side = torch.cuda.Stream()
-        self.p = R.SclkProbe(self.side.cuda_stream, max(1.0, 0.9 * est_ms))
+        self.window_ms = round(max(1.0, 0.9 * est_ms), 3)
+        self.p = R.SclkProbe(self.side.cuda_stream, self.window_ms)
 
     def mhz(self):
         return round(self.p.read(), 1)
+
+
+def warm(fn, n, torch):
+    """Run fn() n (>= 1) times; the wall time of the last one in ms."""
+    for _ in range(max(1, n) - 1):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) * 1e3
 
 
 def world_variant(R, torch, scene, steps, warmup):
@@ -322,11 +336,7 @@ def world_variant(R, torch, scene, steps, warmup):
     rgb = torch.empty((s.height, s.width, 3), dtype=torch.uint8, device="cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     torch.cuda.synchronize()
-    w0 = time.perf_counter()
-    for _ in range(max(1, warmup)):
-        dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st)
-    torch.cuda.synchronize()
-    warm_ms = (time.perf_counter() - w0) / max(1, warmup) * 1e3
+    warm_ms = warm(lambda: dw.render_async(cam, p, ptr, need, rgb.data_ptr(), None, st), warmup, torch)
     timers = [R.Timer() for _ in range(steps)]
     clk = ClockWindow(R, torch, steps * warm_ms)
     a = time.perf_counter()
@@ -344,7 +354,8 @@ def world_variant(R, torch, scene, steps, warmup):
     samples = s.width * s.height * s.spp
     roof = world_roofline(scene, s, ms, info)
     return {"value": round(samples * steps / e / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(e / steps * 1e3, 3),
-            "kernel_ms": round(ms, 3), "sclk_mhz": sclk,
+            "kernel_ms": round(ms, 3), "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
+            "tail_dealing": c["tail_dealing"],
             "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
                                                   "height": s.height, "spp": s.spp, "max_depth": DEPTH},
             "bvh": info, "segments_per_sample": round(c["segments"] / samples, 3),
@@ -384,11 +395,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
                       precision=args.precision, engine="wavefront", **wf_params(args))
     counts = rend.counts(cam, p)  # untimed: the queue / in-register split of the segments
     torch.cuda.synchronize()
-    w0 = time.perf_counter()
-    for _ in range(max(1, args.warmup)):
-        rend.render(cam, p, out=out)
-    torch.cuda.synchronize()
-    warm_ms = (time.perf_counter() - w0) / max(1, args.warmup) * 1e3
+    warm_ms = warm(lambda: rend.render(cam, p, out=out), args.warmup, torch)
     timers = [R.Timer() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -417,7 +424,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
-            "wf_form": args.wf_form, "sclk_mhz": sclk,
+            "wf_form": args.wf_form, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),
@@ -572,13 +579,12 @@ def main():
     counts = rend.counts(cam, R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
                                             precision=args.precision))
     torch.cuda.synchronize()
-    w0 = time.perf_counter()
-    for _ in range(args.warmup):
+
+    def step_warm():
         rend.render(cam, params, out=out)
         if world > 1:
             tg.gather(out)
-    torch.cuda.synchronize()
-    warm_ms = (time.perf_counter() - w0) / max(1, args.warmup) * 1e3
+    warm_ms = warm(step_warm, args.warmup, torch) if args.warmup > 0 else 0.0
 
     # One HIP-event pair per step brackets that step's trace-kernel launch on
     # the render stream (torch's current stream), read after the region.
@@ -651,6 +657,7 @@ def main():
             "traffic": traffic_per_launch(args, W, rc, spp),
             "traffic_source": os.path.relpath(evidence("traffic.json"), REPO),
             "kernel": "trace_kernel", "trace_ms_per_launch": round(trace_ms_avg, 3), "sclk_mhz": sclk,
+            "sclk_window_ms": clk.window_ms if clk is not None else None,
             "flop_per_launch": flops, "segments_per_launch": counts["segments"],
             "hbm": {"achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(hbm_gbs / PEAK_HBM_GBS, 7), "algorithmic_bytes_per_launch": hbm_bytes},

@@ -124,10 +124,11 @@ struct rtw_sclk_probe_s {
 };
 
 namespace {
-// One wave: spin (s_sleep between reads) until `ticks` of the 100-MHz
-// s_memrealtime counter passed; the SIMD clock = delta(s_memtime) / delta(s_memrealtime)
-// x 100 MHz (MI355X_MICROARCH.md: in-kernel clock).  Lane 0 writes the result.
-__global__ void __launch_bounds__(64) sclk_probe_kernel(unsigned long long ticks, double* out) {
+// One wave: spin (s_sleep between reads) until `ticks` of the constant-rate
+// s_memrealtime counter passed; the SIMD clock = delta(s_memtime) /
+// delta(s_memrealtime) x the counter's rate (hipDeviceAttributeWallClockRate,
+// 100 MHz on MI355X; MI355X_MICROARCH.md: in-kernel clock).  Lane 0 writes it.
+__global__ void __launch_bounds__(64) sclk_probe_kernel(unsigned long long ticks, double rt_mhz, double* out) {
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   unsigned long long r = r0;
@@ -136,7 +137,7 @@ __global__ void __launch_bounds__(64) sclk_probe_kernel(unsigned long long ticks
     r = __builtin_amdgcn_s_memrealtime();
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) out[0] = (double)(t1 - t0) / (double)(r - r0) * 100.0;
+  if (threadIdx.x == 0) out[0] = (double)(t1 - t0) / (double)(r - r0) * rt_mhz;
 }
 }  // namespace
 
@@ -1100,13 +1101,19 @@ int rtw_sclk_probe_begin(void* stream, double wall_ms, rtw_sclk_probe* out) {
   if (!out) return fail(RTW_EINVAL, "probe out is NULL");
   *out = nullptr;
   if (!(wall_ms > 0.0 && wall_ms < 600e3)) return fail(RTW_EINVAL, "probe window %g ms outside (0, 600 s)", wall_ms);
+  // the s_memrealtime rate of the current device (kHz), not an assumed 100 MHz
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+    return fail(RTW_EHIP, "probe: wall-clock rate of device %d unavailable", dev);
   auto* p = new rtw_sclk_probe_s;
   p->s = static_cast<hipStream_t>(stream);
   if (hipMalloc(reinterpret_cast<void**>(&p->d), sizeof(double)) != hipSuccess) {
     delete p;
     return fail(RTW_ENOMEM, "probe: hipMalloc failed");
   }
-  hipLaunchKernelGGL(sclk_probe_kernel, dim3(1), dim3(64), 0, p->s, (unsigned long long)(wall_ms * 1e5), p->d);
+  hipLaunchKernelGGL(sclk_probe_kernel, dim3(1), dim3(64), 0, p->s, (unsigned long long)(wall_ms * khz),
+                     (double)khz * 1e-3, p->d);
   if (hipGetLastError() != hipSuccess) {
     (void)hipFree(p->d);
     delete p;

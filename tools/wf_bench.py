@@ -2,8 +2,9 @@
 N renders, HIP events around the bounce loop.
   python tools/wf_bench.py [N] [CFG ...]
 CFG (in-process A/B, configurations interleaved per round): comma-separated
-"paths=<wf_paths>" and environment settings read by the library at each render
-(e.g. "RTW_WF_GRID=4", "RTW_WF_FINISH=0"); "-" is the default configuration."""
+rtw_params fields "paths=<wf_paths>", "sets=<wf_sets>", "drain=samples|slots|none",
+"form=fused|split", and environment settings that only a -DRTW_MEASURE library
+reads (development knobs, e.g. "RTW_WF_GRID=4"); "-" is the default configuration."""
 import os
 import sys
 
@@ -28,14 +29,18 @@ def apply(cfg):
     """Set the configuration's environment; return its params."""
     os.environ.clear()
     os.environ.update(base_env)
-    paths = 0
+    kw = {}
     for kv in ([] if cfg == "-" else cfg.split(",")):
         k, v = kv.split("=")
         if k == "paths":
-            paths = int(v)
+            kw["wf_paths"] = int(v)
+        elif k == "sets":
+            kw["wf_sets"] = int(v)
+        elif k in ("drain", "form"):
+            kw["wf_" + k] = v
         else:
             os.environ[k] = v
-    return R.make_params(W, H, spp, engine="wavefront", wf_paths=paths)
+    return R.make_params(W, H, spp, engine="wavefront", **kw)
 
 
 best = {c: 1e9 for c in cfgs}

@@ -13,7 +13,8 @@ import sys
 fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
 frames = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4].isdigit() else 1
 KERNELS = ("wf_extend", "wf_shade", "wf_step", "wf_finish", "wf_drain")
-FUSED = "--split" not in sys.argv  # the engine form the passes ran (RTW_WF_FUSED)
+FUSED = "--split" not in sys.argv  # the engine form the passes ran (params.wf_form)
+SETS = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--sets=")), 2)  # params.wf_sets
 
 
 def total(d, name):
@@ -33,13 +34,13 @@ wk, wper = total(write_dir, "WRITE_SIZE")
 if fk == 0 or wk == 0:
     sys.exit("no bounce-kernel counter rows")
 res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", "engine": "wavefront",
-                  "fused": FUSED, "sets": int(os.environ.get("RTW_WF_SETS") or 2), "wf_paths": 0},
+                  "fused": FUSED, "sets": SETS, "wf_paths": 0},
        "fetch_size_kb_per_frame": fk / frames, "write_size_kb_per_frame": wk / frames,
        "per_kernel_bytes_per_frame": {k: (2 * fper.get(k, 0.0) + wper.get(k, 0.0)) * 1024 / frames for k in KERNELS},
        "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one 1200x675x500 f64 "
                  "wavefront render (tools/prof_run.py wf64); bytes = 2*FETCH_SIZE + WRITE_SIZE (KB x 1024), "
                  "summed over every bounce launch of the frame (wf_step, or wf_extend + wf_shade) and its in-register "
-                 "drain (wf_drain, or wf_finish with RTW_WF_DRAIN=0)"}
+                 "drain (wf_drain, or wf_finish with params.wf_drain RTW_WF_DRAIN_SLOTS)"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
