@@ -101,6 +101,12 @@ typedef enum {
   RTW_WORLD_FEATURES_AUTO = 0, /* the smallest compiled feature set holding the world's features */
   RTW_WORLD_FEATURES_ALL = 1   /* the general kernel (every primitive, texture and transform) */
 } rtw_world_features;
+typedef enum {
+  RTW_WORLD_TRAVERSAL_AUTO = 0,  /* the default for the world */
+  RTW_WORLD_TRAVERSAL_UNION = 1, /* the wave walks the union of its lanes' BVH paths (scalar node loads) */
+  RTW_WORLD_TRAVERSAL_LANE = 2   /* every lane walks its own path (sphere worlds with a BVH of depth <= 24;
+                                    other worlds take the union walk) */
+} rtw_world_traversal;
 
 typedef struct {
   uint32_t width, height;     /* full image (main.zig:305-306) */
@@ -125,7 +131,7 @@ typedef struct {
   uint32_t world_waves;       /* world kernel: register budget in waves per SIMD (1, 3 or 4),
                                  0 = the feature set's default (4 sphere worlds, 3 rects / transforms, 2 noise) */
   uint32_t world_features;    /* world kernel: rtw_world_features */
-  uint32_t reserved;          /* must be 0 */
+  uint32_t world_traversal;   /* world kernel: rtw_world_traversal */
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u
@@ -353,11 +359,14 @@ int rtw_world_render(const rtw_camera *cam, const rtw_world_desc *desc, const rt
 /* Statistics pass: counts_out[4] = {samples, segments, node_visits, prim_tests}. */
 int rtw_world_render_counts(rtw_world world, const rtw_camera *cam, const rtw_params *params,
                             void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);
-/* The same pass with counts_out[6]: the four above, then the wave iterations
- * of the persistent kernel and whether tail dealing ran (1: the workspace held
- * the per-lane rings, 0: it did not — same image, slower end of launch). */
+/* The same pass with counts_out[8]: the four above (node visits and primitive
+ * tests counted per lane: each lane's own under the per-lane traversal, the
+ * wave's under the union walk), then the wave iterations of the persistent
+ * kernel, whether tail dealing ran (1: the workspace held the per-lane rings,
+ * 0: it did not — same image, slower end of launch), and the per-lane
+ * traversal's interior-step and leaf-test wave iterations (0 for the union). */
 int rtw_world_render_counts_ex(rtw_world world, const rtw_camera *cam, const rtw_params *params,
-                               void *workspace, size_t workspace_bytes, uint64_t counts_out[6]);
+                               void *workspace, size_t workspace_bytes, uint64_t counts_out[8]);
 
 #ifdef __cplusplus
 }

@@ -245,6 +245,10 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kCullBit = 0x40000000u;  // leaf ref: pretest record present
 constexpr uint32_t kLeafCountMask = 0x7Fu;  // leaf ref: count = (ref >> 23) & mask
 constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder caps the depth)
+// per-LANE stack entries of the per-lane traversal (rtw_world.hip closest_lane):
+// a BVH of depth <= kLaneStack never overflows it (a push per level at most);
+// deeper BVHs take the union walk
+constexpr uint32_t kLaneStack = 24;
 #ifndef RTW_MAX_LEAF_PRIMS
 #define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
 #endif
@@ -277,12 +281,13 @@ struct WorldArgs {
 constexpr uint32_t kTailWin = 32;  // world kernel: the last samples of a unit other lanes may trace (ring entries)
 
 // occ: register-allocation target (workgroups per CU): 1 (none), 3 or 4.
-// fs: the kernel's feature set, world_feature_set(features of the world):
-// bits 1 noise texture, 2 image texture, 4 transform chains, 8 rects.
-int world_feature_set(uint32_t feat);
+// fs: the kernel's feature set, world_feature_set(features of the world, per-lane
+// traversal): bits 1 noise texture, 2 image texture, 4 transform chains, 8 rects,
+// 16 per-lane BVH traversal (sphere worlds only).
+int world_feature_set(uint32_t feat, bool lane);
 hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs);
 int world_blocks_per_cu(size_t lds, int occ, int fs);
 constexpr int kWorldBlock = 256;
-size_t world_lds_bytes(uint32_t n_perlins);
+size_t world_lds_bytes(uint32_t n_perlins, int fs);
 
 }  // namespace rtwk

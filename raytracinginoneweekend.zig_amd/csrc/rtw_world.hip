@@ -58,6 +58,9 @@ using V = V3<D>;
 // transform chains or rects (the budget sets the spills at 4 waves/SIMD).
 constexpr int kFeatNoise = 1, kFeatImage = 2, kFeatXform = 4, kFeatRect = 8;
 constexpr int kFeatAll = kFeatNoise | kFeatImage | kFeatXform | kFeatRect;
+// Not a world feature: the sphere-world instantiation that traverses the BVH
+// per lane (closest_lane) instead of as the wave's union (closest).
+constexpr int kFeatLane = 16;
 
 __device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
 
@@ -341,7 +344,7 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
       if (ok) accept(h, t, (int)k, (int)q.orig, tmin);
     };
     bool need0 = true, need1 = true;
-    if ((FEAT & ~kFeatImage) == 0 && (ref & kCullBit)) {  // sphere worlds (the other sets ignore the bit)
+    if ((FEAT & ~(kFeatImage | kFeatLane)) == 0 && (ref & kCullBit)) {  // sphere worlds (the others ignore the bit)
       const f2 x = cull_pair<1>(ld_pair(ct, first), bc((float)o.x), bc((float)o.y), bc((float)o.z), bc((float)d.x),
                                 bc((float)d.y), bc((float)d.z), bc(lk.na), bc(lk.k), bc((float)time));
       need0 = (act & ~(cull_ok & wballot(x.x < 0.0f))) != 0;  // some lane not proven to miss
@@ -433,6 +436,121 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
   }
 }
 
+// Per-lane BVH traversal (sphere worlds, FEAT & kFeatLane; VERDICT r4 ask 2):
+// every lane walks its OWN path through the tree — its own stack (a column of
+// this wave's LDS block, entry e of lane l at e * 64 + l: conflict-free),
+// its own node loads (per-lane vector loads; the 371-KB globe BVH stays in
+// L2), nearer child first by its own entry distance — instead of the wave
+// walking the union of its 64 lanes' paths (86.6 wave-level node visits per
+// segment on the globe against 15.8 per lane).  While-while structure: the
+// lanes holding an interior node step until every lane holds a leaf or is
+// done, then every lane at a leaf tests its <= 2 primitives; the loop runs to
+// the wave's longest path, not to the union.  Same slab arithmetic, margins
+// and inclusive bounds as the union walk, the same
+// order-independent acceptance (§5.1) and NaN fallback, so the same winner.
+template <int MODE, int FEAT, typename WV>
+__device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack, uint32_t lid, const V& o,
+                                             const V& d, D time, D tmin, WHit& h, unsigned long long& nv,
+                                             unsigned long long& nt, unsigned long long& wi, unsigned long long& wl) {
+  h.pos = -1;
+  h.orig = -1;
+  h.t = (D)__builtin_huge_val();
+  h.nan = 0u;
+  const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
+  const f2 ix = bc((float)inv.x), iy = bc((float)inv.y), iz = bc((float)inv.z);
+  const float mf = (float)m;
+  const float pxo = -(float)o.x * ix[0], pyo = -(float)o.y * iy[0], pzo = -(float)o.z * iz[0];
+  const float mx = mf * fabsf(ix[0]), my = mf * fabsf(iy[0]), mz = mf * fabsf(iz[0]);
+  const float sx = ix[0] < 0.0f ? -1.0f : 1.0f, sy = iy[0] < 0.0f ? -1.0f : 1.0f, sz = iz[0] < 0.0f ? -1.0f : 1.0f;
+  const f2 oxl = bc(pxo - sx * mx), oxh = bc(pxo + sx * mx);
+  const f2 oyl = bc(pyo - sy * my), oyh = bc(pyo + sy * my);
+  const f2 ozl = bc(pzo - sz * mz), ozh = bc(pzo + sz * mz);
+  const float tminf = next_down((float)tmin);
+  auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
+  float tmaxf = round_up(h.t);
+  const D* pr = W.prim;
+  const RaySp ws = ray_space(o, d, W.flags);
+  constexpr uint32_t kNoRef = 0xFFFFFFFFu;  // (never a ref: interior refs < kLeafBit, leaf counts <= 2)
+  // per lane: the node (or leaf) to process next, a postponed leaf, the stack
+  // depth; the stack's top entry lives in a register (`top`, kNoRef when the
+  // stack is empty; entries below it in LDS), so a pop waits on no LDS read:
+  // the next top's read is issued at the pop and lands during the node visit.
+  uint32_t ref = 0u, pend = kNoRef, sp = 0u, top = kNoRef;
+  auto pop = [&]() -> uint32_t {
+    const uint32_t r = top;
+    top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
+    return r;
+  };
+  auto push = [&](uint32_t r) {
+    if (top != kNoRef) lstack[(sp++) * 64u + lid] = top;
+    top = r;
+  };
+  for (;;) {
+    // Interior steps.  A lane that reaches a leaf postpones it (one slot) and
+    // keeps traversing; the phase ends once every lane holds a leaf or is out
+    // of work (Aila & Laine's speculative while-while): the leaf tests then
+    // run with most lanes busy.
+    for (;;) {
+      const bool step = ref < kLeafBit;
+      if (!wany(step & (pend == kNoRef))) break;
+      if (MODE == 1 && lid == 0) ++wi;
+      if (step) {
+        if (MODE == 1) ++nv;
+        const float4* nd = reinterpret_cast<const float4*>(W.node + (size_t)ref * kNodeWords);
+        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3, refs in words 12-13
+        const f2 x0 = pfma(f2{q0.x, q0.y}, ix, oxl), x1 = pfma(f2{q1.z, q1.w}, ix, oxh);
+        const f2 y0 = pfma(f2{q0.z, q0.w}, iy, oyl), y1 = pfma(f2{q2.x, q2.y}, iy, oyh);
+        const f2 z0 = pfma(f2{q1.x, q1.y}, iz, ozl), z1 = pfma(f2{q2.z, q2.w}, iz, ozh);
+        float tn[2];
+        bool hit[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), max_q(fminf(z0[c], z1[c]), tminf));
+          const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), min_q(fmaxf(z0[c], z1[c]), tmaxf));
+          tn[c] = n;
+          hit[c] = n <= f;
+        }
+        const uint32_t r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
+        const bool first0 = tn[0] <= tn[1];
+        uint32_t nx = hit[0] ? r0 : (hit[1] ? r1 : kNoRef);
+        if (hit[0] && hit[1]) {
+          push(first0 ? r1 : r0);
+          nx = first0 ? r0 : r1;
+        }
+        ref = nx != kNoRef ? nx : pop();
+        if (ref != kNoRef && ref >= kLeafBit && pend == kNoRef) {  // postpone the leaf, keep walking
+          pend = ref;
+          ref = pop();
+        }
+      }
+    }
+    // Leaf tests: the postponed leaf, else a leaf the lane stopped at.
+    uint32_t lf = pend;
+    if (lf == kNoRef && ref != kNoRef && ref >= kLeafBit) {
+      lf = ref;
+      ref = pop();
+    }
+    pend = kNoRef;
+    if (!wany(lf != kNoRef)) {
+      if (!wany(ref != kNoRef)) break;
+      continue;
+    }
+    if (MODE == 1 && lid == 0) ++wl;
+    static_assert(kMaxLeafPrims <= 2, "closest_lane tests leaves of <= 2 primitives");
+    if (lf != kNoRef) {  // 1 or 2 primitives (kMaxLeafPrims): both records loaded before either test
+      const uint32_t first = lf & 0x7FFFFFu, cnt = (lf >> 23) & kLeafCountMask;
+      const PrimRec q0 = load_rec(pr + kWorldRec * first);
+      const PrimRec q1 = load_rec(pr + kWorldRec * (cnt > 1u ? first + 1u : first));
+      D t;
+      if (MODE == 1) nt += cnt;
+      if (root_obj<true, FEAT>(q0, ws, time, tmin, t)) accept(h, t, (int)first, (int)q0.orig, tmin);
+      if (cnt > 1u && root_obj<true, FEAT>(q1, ws, time, tmin, t)) accept(h, t, (int)first + 1, (int)q1.orig, tmin);
+      tmaxf = round_up(h.t);
+    }
+  }
+}
+
 // Texture.value (texture.zig:36-144) for the winner's record.
 template <int FEAT, typename WV>
 __device__ __forceinline__ V tex_value(const WV& W, uint32_t ti, D u, D v, V p) {
@@ -499,7 +617,10 @@ __device__ __forceinline__ V tex_value(const WV& W, uint32_t ti, D u, D v, V p) 
 template <int MODE, int OCC, int FEAT>
 __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kBvhStack;  // this wave's stack
+  // this wave's BVH stack: one column per lane (per-lane traversal) or one
+  // wave-uniform stack (the union walk)
+  uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) +
+                    (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? kLaneStack * 64u : kBvhStack);
   // Tail dealing rows of this wave's lanes (lane = the owner of a unit): the
   // first sample handed to other lanes (samples [hi, s_end) are theirs), the
   // ring entries they filled, the unit's pixel; and the dealing list.
@@ -552,6 +673,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   LaneFlag<16u> helping{lane_flags};  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
+  unsigned long long n_wi = 0, n_wl = 0;  // per-lane traversal: interior / leaf wave iterations
   KStats st;  // MODE 2: phase stamps
   if constexpr (MODE == 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st.t_last)::"memory");
   // The loop body, compiled twice: without the tail dealing for the bulk of
@@ -672,7 +794,11 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         if (MODE == 1) ++n_segments;
         WHit h;
         WSTAMP(1)  // sample start (+ take units, loop control)
-        closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
+        if constexpr ((FEAT & kFeatLane) != 0)
+          closest_lane<MODE, FEAT>(W, WKA(margin), stack, lid, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests,
+                                   n_wi, n_wl);
+        else
+          closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
         if (__builtin_expect(h.nan != 0u, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
         if (h.pos < 0) {  // miss: background (main.zig:109-112)
           const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
@@ -879,10 +1005,16 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     atomicAdd(A.counts + 2, n_visits);
     atomicAdd(A.counts + 3, n_tests);
     if (lid == 0) atomicAdd(A.counts + 4, n_iters);
+    if ((FEAT & kFeatLane) && lid == 0) {
+      atomicAdd(A.counts + 5, n_wi);
+      atomicAdd(A.counts + 6, n_wl);
+    }
   }
 }
 
-size_t world_lds_bytes(uint32_t) { return (size_t)kBvhStack * (kWorldBlock / 64) * sizeof(uint32_t); }
+size_t world_lds_bytes(uint32_t, int fs) {
+  return (size_t)((fs & kFeatLane) ? kLaneStack * 64u : kBvhStack) * (kWorldBlock / 64) * sizeof(uint32_t);
+}
 
 template <int OCC, int FEAT>
 static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode) {
@@ -909,13 +1041,15 @@ static void launch_feat(const WorldArgs& a, uint32_t grid, size_t lds, hipStream
 // Instantiated feature sets: spheres with solid / checker / image textures
 // (scenes 1, 2, 4 and configs[4]'s globe), rects + transforms + lights without
 // noise / image (the Cornell box, scene 5's light), and everything.
-int world_feature_set(uint32_t feat) {
-  if ((feat & ~(uint32_t)kFeatImage) == 0u) return kFeatImage;
+int world_feature_set(uint32_t feat, bool lane) {
+  if ((feat & ~(uint32_t)kFeatImage) == 0u) return lane ? (kFeatImage | kFeatLane) : kFeatImage;
   if ((feat & ~(uint32_t)(kFeatXform | kFeatRect)) == 0u) return kFeatXform | kFeatRect;
   return kFeatAll;
 }
 hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs) {
-  if (fs == kFeatImage)
+  if (fs == (kFeatImage | kFeatLane))
+    launch_feat<kFeatImage | kFeatLane>(a, grid, lds, s, mode, occ);
+  else if (fs == kFeatImage)
     launch_feat<kFeatImage>(a, grid, lds, s, mode, occ);
   else if (fs == (kFeatXform | kFeatRect))
     launch_feat<kFeatXform | kFeatRect>(a, grid, lds, s, mode, occ);
@@ -937,6 +1071,7 @@ static int bpc_feat(size_t lds, int occ) {
   return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 int world_blocks_per_cu(size_t lds, int occ, int fs) {
+  if (fs == (kFeatImage | kFeatLane)) return bpc_feat<kFeatImage | kFeatLane>(lds, occ);
   if (fs == kFeatImage) return bpc_feat<kFeatImage>(lds, occ);
   if (fs == (kFeatXform | kFeatRect)) return bpc_feat<kFeatXform | kFeatRect>(lds, occ);
   return bpc_feat<kFeatAll>(lds, occ);

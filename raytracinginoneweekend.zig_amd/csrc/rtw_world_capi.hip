@@ -576,17 +576,22 @@ struct WorldLaunchCfg {
 };
 WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   WorldLaunchCfg c;
-  c.lds = rtwk::world_lds_bytes(w->view.n_perlins);
+  // Kernel instantiation for the world's features (params.world_features
+  // RTW_WORLD_FEATURES_ALL: the general kernel; every set gives the same bits)
+  // and its BVH traversal (params.world_traversal): per lane for sphere worlds
+  // whose BVH fits the per-lane stack, else the wave's union walk.
+  const uint32_t feat = p->world_features == RTW_WORLD_FEATURES_ALL ? 15u : w->feat;
+  const bool lane = p->world_traversal == RTW_WORLD_TRAVERSAL_LANE && w->view.n_nodes > 0 &&
+                    w->info[2] <= rtwk::kLaneStack && w->info[3] <= 2u;
+  c.fs = rtwk::world_feature_set(feat, lane);
+  c.lds = rtwk::world_lds_bytes(w->view.n_perlins, c.fs);
   // Register-allocation target in waves per SIMD (params.world_waves, 0 = the
   // feature set's default).
   const int occ = p->world_waves ? (int)p->world_waves : world_occ_default(w);
-  // Kernel instantiation for the world's features (params.world_features
-  // RTW_WORLD_FEATURES_ALL: the general kernel; every set gives the same bits).
-  c.fs = rtwk::world_feature_set(p->world_features == RTW_WORLD_FEATURES_ALL ? 15u : w->feat);
   c.oi = occ >= 4 ? 4 : (occ == 3 ? 3 : 1);
   static std::mutex mu;
-  static int bpc_cache[16][5] = {};
-  static size_t bpc_lds[16][5] = {};
+  static int bpc_cache[32][5] = {};
+  static size_t bpc_lds[32][5] = {};
   int bpc;
   {
     std::lock_guard<std::mutex> lk(mu);
@@ -669,7 +674,7 @@ int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params
 }
 
 int rtw_world_render_counts_ex(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
-                               uint64_t counts_out[6]) {
+                               uint64_t counts_out[8]) {
   if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
 #ifdef RTW_MEASURE
   // RTW_WORLD_PHASE=1 (diagnostic build): a phase-stamp pass first; its wave-cycle
@@ -693,19 +698,21 @@ int rtw_world_render_counts_ex(rtw_world w, const rtw_camera* cam, const rtw_par
   const int st = world_launch(w, cam, p, ws, ws_bytes, nullptr, nullptr, nullptr, nullptr, 1, &tail);
   if (st != RTW_OK) return st;
   if (hipDeviceSynchronize() != hipSuccess) return rtw_fail(RTW_EHIP, "world counts pass failed");
-  unsigned long long c[5];
+  unsigned long long c[7];
   if (hipMemcpy(c, static_cast<unsigned char*>(ws) + rtw_ws_stats_off(p), sizeof(c), hipMemcpyDeviceToHost) !=
       hipSuccess)
     return rtw_fail(RTW_EHIP, "counts copy failed");
   for (int i = 0; i < 5; ++i) counts_out[i] = c[i];  // samples, segments, node visits, primitive tests, wave iterations
   counts_out[5] = tail;
+  counts_out[6] = c[5];  // per-lane traversal: interior-step wave iterations
+  counts_out[7] = c[6];  // and leaf-test wave iterations
   return RTW_OK;
 }
 
 int rtw_world_render_counts(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,
                             uint64_t counts_out[4]) {
   if (!counts_out) return rtw_fail(RTW_EINVAL, "counts is NULL");
-  uint64_t c[6];
+  uint64_t c[8];
   const int st = rtw_world_render_counts_ex(w, cam, p, ws, ws_bytes, c);
   if (st == RTW_OK)
     for (int i = 0; i < 4; ++i) counts_out[i] = c[i];

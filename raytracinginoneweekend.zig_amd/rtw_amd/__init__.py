@@ -33,6 +33,7 @@ DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (params.wf_sets overrides)
 WF_DRAIN = {"samples": 0, "slots": 1, "none": 2}  # rtw_wf_drain
 WF_FORM = {"fused": 0, "split": 1}  # rtw_wf_form
 WORLD_FEATURES = {"auto": 0, "all": 1}  # rtw_world_features
+WORLD_TRAVERSAL = {"auto": 0, "union": 1, "lane": 2}  # rtw_world_traversal
 STATS_WORDS = 16  # rtw_hip.h RTW_STATS_WORDS
 STAT_NAMES = ["samples", "segments", "f32_skips", "cand_wave_iters", "cand_lanes", "disc_ge0_lanes",
               "sphere_loop_wave_iters", "cull_survivor_lanes", "cull_exact_wave_iters", "drain_segments",
@@ -70,7 +71,7 @@ class Params(C.Structure):
                 ("chunk", C.c_uint32), ("precision", C.c_uint32), ("device", C.c_int32),
                 ("engine", C.c_uint32), ("wf_paths", C.c_uint32),
                 ("wf_sets", C.c_uint32), ("wf_drain", C.c_uint32), ("wf_form", C.c_uint32),
-                ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("reserved", C.c_uint32)]
+                ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("world_traversal", C.c_uint32)]
 
 
 _lib = None
@@ -177,7 +178,7 @@ def cover_scene(seed: int = 42):
 def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACKGROUND, row_begin=0,
                 row_stride=1, row_count=None, chunk=0, precision="f64", device=-1, engine="megakernel",
                 wf_paths=0, wf_sets=0, wf_drain="samples", wf_form="fused", world_waves=0,
-                world_features="auto") -> Params:
+                world_features="auto", world_traversal="auto") -> Params:
     """rtw_params (ABI v4): every engine choice is a field (0 / the first
     name = the library default); nothing is read from the environment."""
     if row_count is None:
@@ -189,7 +190,8 @@ def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACK
         return names[v] if isinstance(v, str) else int(v)
     return Params(width, height, spp, max_depth, seed, (C.c_double * 3)(*background), row_begin, row_stride,
                   row_count, chunk, prec, device, eng, wf_paths, wf_sets, enum(wf_drain, WF_DRAIN),
-                  enum(wf_form, WF_FORM), world_waves, enum(world_features, WORLD_FEATURES), 0)
+                  enum(wf_form, WF_FORM), world_waves, enum(world_features, WORLD_FEATURES),
+                  enum(world_traversal, WORLD_TRAVERSAL))
 
 
 def _arr(x, typ):

@@ -93,7 +93,7 @@ def _wlib():
     L.rtw_world_render_counts.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                           C.c_uint64 * 4]
     L.rtw_world_render_counts_ex.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
-                                             C.c_uint64 * 6]
+                                             C.c_uint64 * 8]
     L._world_ready = True
     return L
 
@@ -302,11 +302,12 @@ class DeviceWorld:
     def counts(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int) -> dict:
         """rtw_world_render_counts_ex: the counts, the persistent kernel's wave
         iterations and whether tail dealing ran (the workspace held the rings)."""
-        out = (C.c_uint64 * 6)()
+        out = (C.c_uint64 * 8)()
         _check(_wlib().rtw_world_render_counts_ex(self.h, C.byref(cam), C.byref(params),
                                                   C.c_void_p(workspace_ptr), workspace_bytes_, out))
         return {"samples": int(out[0]), "segments": int(out[1]), "node_visits": int(out[2]),
-                "prim_tests": int(out[3]), "wave_iters": int(out[4]), "tail_dealing": bool(out[5])}
+                "prim_tests": int(out[3]), "wave_iters": int(out[4]), "tail_dealing": bool(out[5]),
+                "lane_interior_iters": int(out[6]), "lane_leaf_iters": int(out[7])}
 
     def close(self):
         if self.h:

@@ -39,12 +39,14 @@ def oracle_world_from_desc(oracle, W, b, earth=None):
                              background=b.background)
 
 
-@pytest.mark.parametrize("scene,w,spp", [(1, 96, 4), (2, 96, 4), (3, 96, 4), (4, 96, 4), (5, 96, 8), (6, 64, 8)])
-def test_world_scene_parity(rtw, oracle, W, earth, scene, w, spp):
+@pytest.mark.parametrize("scene,w,spp,trav", [(1, 96, 4, "union"), (1, 96, 4, "lane"), (2, 96, 4, "union"),
+                                              (3, 96, 4, "union"), (4, 96, 4, "union"), (5, 96, 8, "union"),
+                                              (6, 64, 8, "union")])
+def test_world_scene_parity(rtw, oracle, W, earth, scene, w, spp, trav):
     b = built(W, scene, earth)
     cam = b.camera()
     h = rtw.image_height(w, b.settings.aspect)
-    g = W.render_world(cam, b.desc, params(rtw, b, w, h, spp))
+    g = W.render_world(cam, b.desc, params(rtw, b, w, h, spp, world_traversal=trav))
     o = oracle.OracleWorld(scene, 42, image=earth if scene in (4, 7) else None)
     ref, _ = o.render_tier_b(o.camera(), w, h, spp)
     assert_parity(g, ref, f"world scene {scene} {w}x{h}x{spp}")
@@ -61,16 +63,21 @@ def test_world_scene1_equals_megakernel(rtw, W, earth):
     assert np.array_equal(mkm.view(np.uint32), wdm.view(np.uint32))
 
 
-def test_world_globe_parity(rtw, oracle, W, earth):
+TRAVERSALS = ["union", "lane"]  # rtw_params.world_traversal: the wave's union walk / per-lane walks
+
+
+@pytest.mark.parametrize("trav", TRAVERSALS)
+def test_world_globe_parity(rtw, oracle, W, earth, trav):
     b = built(W, 7, earth)
     cam = b.camera()
-    g = W.render_world(cam, b.desc, params(rtw, b, 64, 36, 2))
+    g = W.render_world(cam, b.desc, params(rtw, b, 64, 36, 2, world_traversal=trav))
     o = oracle.OracleWorld(7, 42, image=earth)
     ref, _ = o.render_tier_b(o.camera(), 64, 36, 2)
     assert_parity(g, ref, "globe 64x36x2")
 
 
-def test_globe_config4_workload_equals_oracle(rtw, oracle, W, earth):
+@pytest.mark.parametrize("trav", TRAVERSALS)
+def test_globe_config4_workload_equals_oracle(rtw, oracle, W, earth, trav):
     """BASELINE configs[4] at its bench workload: the globe + 10k-sphere frame
     at 1200x675x100 through the BVH (leaf pretest, outward-rounded f32 slabs:
     conservative bounds whose failure mode is a rare dropped hit).  16 rows
@@ -87,13 +94,13 @@ def test_globe_config4_workload_equals_oracle(rtw, oracle, W, earth):
     assert (s.width, s.height, s.spp) == (1200, 675, 100)
     cam = b.camera()
     t0 = time.time()
-    g = W.render_world(cam, b.desc, params(rtw, b, s.width, s.height, s.spp))
+    g = W.render_world(cam, b.desc, params(rtw, b, s.width, s.height, s.spp, world_traversal=trav))
     t_gpu = time.time() - t0
     fx = np.load(os.path.join(GOLDEN, "globe_1200x675x100_rows7s42.npz"))
     rows = fx["rows"]
     assert len(rows) == 16 and int(fx["samples"]) == 16 * 1200 * 100
     d = diff_stats(g[rows], fx["rgb"])
-    print(f"globe 1200x675x100 (GPU {t_gpu:.1f} s incl. upload + BVH build) vs fixture rows 7::42:", d)
+    print(f"globe 1200x675x100 {trav} (GPU {t_gpu:.1f} s incl. upload + BVH build) vs fixture rows 7::42:", d)
     assert d["max"] == 0, d  # bit-identical
     o = oracle.OracleWorld(7, 42, image=earth)
     t0 = time.time()
@@ -164,21 +171,25 @@ def _render_dev(rtw, W, b, cam, p, linear):
     return rgb.cpu().numpy(), mean.cpu().numpy(), counts, info
 
 
+@pytest.mark.parametrize("trav", TRAVERSALS)
 @pytest.mark.parametrize("scene,w,spp", [(7, 320, 4), (1, 160, 8)])
-def test_world_bvh_equals_linear(rtw, W, earth, scene, w, spp):
+def test_world_bvh_equals_linear(rtw, W, earth, scene, w, spp, trav):
     b = built(W, scene, earth)
     cam = b.camera()
     h = rtw.image_height(w, b.settings.aspect)
-    p = params(rtw, b, w, h, spp)
+    p = params(rtw, b, w, h, spp, world_traversal=trav)
     rb, mb, cb, info = _render_dev(rtw, W, b, cam, p, linear=False)
     rl, ml, cl, _ = _render_dev(rtw, W, b, cam, p, linear=True)
     assert (rb == rl).all() and np.array_equal(mb.view(np.uint32), ml.view(np.uint32)), diff_stats(rb, rl)
     assert cb["samples"] == cl["samples"] == w * h * spp
     assert cb["segments"] == cl["segments"]
-    print(scene, info, "prim tests bvh/linear", cb["prim_tests"], cl["prim_tests"])
+    print(scene, trav, info, "prim tests bvh/linear", cb["prim_tests"], cl["prim_tests"],
+          "node visits per segment", cb["node_visits"] / cb["segments"])
     assert info["nodes"] > 0  # worlds of > 32 primitives get a BVH
     if scene == 7:
         assert info["max_depth"] <= 32 and cb["prim_tests"] * 50 < cl["prim_tests"]
+        if trav == "lane":  # each lane's own walk (VERDICT r4 ask 2: <= 25 node visits per lane-segment)
+            assert cb["lane_interior_iters"] > 0 and cb["node_visits"] <= 25 * cb["segments"]
 
 
 @pytest.mark.parametrize("scene,w,spp", [(7, 160, 2), (3, 96, 2), (6, 64, 4)])

@@ -38,9 +38,10 @@ for line in open(f"{root}/wpmc_{scene}_b.log"):
 segments = run["segments_per_sample"] * run["W"] * run["H"] * run["spp"]
 cyc = c["GRBM_GUI_ACTIVE"] / 8  # per-XCD counter summed over the 8 XCDs
 clock = cyc / (ms * 1e-3)
-out = {"what": f"PMC passes of ONE world_kernel dispatch (scene {scene}, {run['name']}, {run['W']}x{run['H']}x"
+out = {"what": f"PMC passes of ONE world_kernel dispatch (scene {run['scene']}, {run['name']}, {run['W']}x{run['H']}x"
                f"{run['spp']}), rocprofv3 --pmc, one pass per counter set (tools/gpu_world_pmc.sh)",
-       "scene": int(scene), "kernel": kernel, "dispatch_ms": ms, "clock_ghz": round(clock / 1e9, 3),
+       "scene": run["scene"], "config": {k: run[k] for k in ("world_traversal", "world_waves") if k in run},
+       "kernel": kernel, "dispatch_ms": ms, "clock_ghz": round(clock / 1e9, 3),
        "segments": round(segments), "counters": {k: c[k] for k in sorted(c)},
        "valu_per_wave_iteration": round(c["SQ_INSTS_VALU"] / (segments / 64)),
        "salu_per_wave_iteration": round(c["SQ_INSTS_SALU"] / (segments / 64)),
