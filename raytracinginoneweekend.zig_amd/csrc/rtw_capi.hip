@@ -798,6 +798,7 @@ struct WfSet {
 // launches: every wave reads its count first.  Sets run on their own streams,
 // forked from and joined back to the caller's stream.
 constexpr uint32_t kWfBatch = 64;
+constexpr uint32_t kWfBounces = 1;
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
 int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned char* ws, const WsLayout& L, int dev,
@@ -814,6 +815,10 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // runs dry.
   const char* be = dev_knob("RTW_WF_BATCH");
   const uint32_t refill = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
+  // Bounce segments per path per wf_step launch (kWfBounces; development knob
+  // RTW_WF_BOUNCES): the path stays in registers between them.
+  const char* bo = dev_knob("RTW_WF_BOUNCES");
+  const uint32_t bounces = (bo && *bo) ? (uint32_t)std::max(1, atoi(bo)) : kWfBounces;
   // Persistent grids: every resident wave slot of each bounce kernel (at most
   // one wave per segment); the same grids for every launch of the frame.
   // The drains always run max_grid = ceil(segs / waves per block) blocks: one
@@ -865,6 +870,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     a.n_slots = (uint32_t)n;
     a.n_segs = segs;
     a.batch = refill;
+    a.bounces = bounces;
     S.s = k == 0 ? stream : wf_side_stream(dev, k);  // (set 0: the caller's stream, NULL = the default stream)
     if (k > 0 && !S.s) {
       st = fail(RTW_EHIP, "wavefront side stream creation failed");

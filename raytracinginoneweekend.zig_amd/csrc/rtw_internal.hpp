@@ -189,6 +189,7 @@ struct WfArgs {
                        // sample's radiance is an R value; widened to f64 when folded, as the other engines add it)
   uint32_t n_slots, n_segs;
   uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
+  uint32_t bounces;    // wf_step: bounce segments per path per launch (>= 1), the path kept in registers between them
 };
 
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);
@@ -248,7 +249,7 @@ constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder c
 // per-LANE stack entries of the per-lane traversal (rtw_world.hip closest_lane):
 // a BVH of depth <= kLaneStack never overflows it (a push per level at most);
 // deeper BVHs take the union walk
-constexpr uint32_t kLaneStack = 24;
+constexpr uint32_t kLaneStack = 16;
 #ifndef RTW_MAX_LEAF_PRIMS
 #define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
 #endif
@@ -277,6 +278,7 @@ struct WorldArgs {
   unsigned long long* counts;  // stats pass: {samples, segments, node visits, prim tests}
   double* ring;         // tail dealing: [lane of the grid][kTailWin][3] radiance of samples traced for that lane's unit
   uint32_t tail_deal;   // 1: lanes the queue left without a unit trace samples of the wave's other units
+  uint32_t lane_yield;  // per-lane traversal: a phase pauses once fewer lanes than this still walk (0: never)
 };
 constexpr uint32_t kTailWin = 32;  // world kernel: the last samples of a unit other lanes may trace (ring entries)
 

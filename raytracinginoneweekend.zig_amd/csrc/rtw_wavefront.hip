@@ -489,10 +489,20 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
       hit = A.in.hk[i];
       tmax = A.in.ht[i];
     }
-    const bool live = shade_step<R, F32, STATS>(A, T, lid, valid, L, slot, hit, tmax, qnext, qend);
-    int nh = -1;
-    R nt = (R)__builtin_huge_val();
-    if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
+    // A.bounces (>= 1) bounce segments per path in this launch: shade, then
+    // the next ray's closest hit, with the path kept in registers between
+    // them (one queue read and one write per A.bounces segments; the same
+    // per-sample arithmetic in the same order, so the same bits).
+    bool live = valid;
+    int nh = hit;
+    R nt = tmax;
+    for (uint32_t b = 0; b < A.bounces; ++b) {
+      live = shade_step<R, F32, STATS>(A, T, lid, live, L, slot, nh, nt, qnext, qend);
+      nh = -1;
+      nt = (R)__builtin_huge_val();
+      if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
+      if (!wany(live)) break;
+    }
     push_path_hit(A.out, base, out_n, live, L, slot, nh, nt);
     if (lid == 0) {
       A.seg_out[seg] = out_n;
@@ -566,8 +576,8 @@ __global__ void __launch_bounds__(kTraceBlock) wf_finish(WfArgs<R> A) {
 // A unit done publishes its chunk sum; its slot then takes the next unit from
 // the segment's reservoir / the device queue (retiring when there is none),
 // so the kernel is correct whenever it runs, as wf_finish — provided the grid
-// holds one wave per segment (it has no segment loop; the host launches
-// exactly that grid and refuses a smaller one, rtw_capi.hip run_wavefront).
+// holds one wave per segment (it has no segment loop; the host always launches
+// ceil(segments / waves per block) blocks, rtw_capi.hip run_wavefront).
 struct DrainUnit {  // 64 B per slot
   uint32_t unit, next, end, fold;  // unit id, next sample to deal, sample end, next sample to fold
   uint32_t ready, miss, live, pad; // ring bits (sample % kDrainWin): radiance stored / sample missed; unit held

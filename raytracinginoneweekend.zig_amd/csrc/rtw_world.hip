@@ -442,20 +442,60 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
 // its own node loads (per-lane vector loads; the 371-KB globe BVH stays in
 // L2), nearer child first by its own entry distance — instead of the wave
 // walking the union of its 64 lanes' paths (86.6 wave-level node visits per
-// segment on the globe against 15.8 per lane).  While-while structure: the
-// lanes holding an interior node step until every lane holds a leaf or is
-// done, then every lane at a leaf tests its <= 2 primitives; the loop runs to
-// the wave's longest path, not to the union.  Same slab arithmetic, margins
-// and inclusive bounds as the union walk, the same
+// segment on the globe against ~16 per lane).  While-while structure with
+// speculative leaves (Aila & Laine): the lanes holding an interior node step
+// until every lane holds a leaf (postponed, one per lane) or is out of work,
+// then every lane at a leaf tests its <= 2 primitives.  Same slab arithmetic,
+// margins and inclusive bounds as the union walk, the same
 // order-independent acceptance (§5.1) and NaN fallback, so the same winner.
+//
+// Resumable: a wave's traversal loop runs to its longest path, so the phase
+// YIELDS once fewer than `yield_lanes` of its lanes are still walking (and
+// the wave has other work): the walking lanes keep their state (node, leaf,
+// stack, closest hit: LaneTrav rows in LDS) and continue in the next
+// iteration of the persistent loop, while the others shade their hits and
+// start their next segments (dynamic ray fetch).  No result depends on when a
+// walk pauses.
+constexpr uint32_t kNoRef = 0xFFFFFFFFu;  // (never a ref: interior refs < kLeafBit, leaf counts <= 2)
+constexpr uint32_t kTravWords = 10;       // LaneTrav rows: ref, pend, top, sp, tmaxf, pos, orig, nan, t (2)
+struct LaneTravRows {                     // one wave's rows, [field][lane]
+  uint32_t w[kTravWords][64];
+};
+// Starts a walk from the root for this lane (no hit yet).
+__device__ __forceinline__ void trav_begin(LaneTravRows* R, uint32_t lid) {
+  R->w[0][lid] = 0u;  // the root node
+  R->w[1][lid] = kNoRef;
+  R->w[2][lid] = kNoRef;
+  R->w[3][lid] = 0u;
+  R->w[4][lid] = __float_as_uint(__builtin_inff());
+  R->w[5][lid] = 0xFFFFFFFFu;  // pos -1
+  R->w[6][lid] = 0xFFFFFFFFu;  // orig -1
+  R->w[7][lid] = 0u;
+  const uint64_t tb = __builtin_bit_cast(uint64_t, (D)__builtin_huge_val());
+  R->w[8][lid] = (uint32_t)tb;
+  R->w[9][lid] = (uint32_t)(tb >> 32);
+}
+// One traversal phase of the lanes with `walking` set; returns true for the
+// lanes whose walk finished in it (`h` = the closest hit).  Wave-converged.
 template <int MODE, int FEAT, typename WV>
-__device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack, uint32_t lid, const V& o,
-                                             const V& d, D time, D tmin, WHit& h, unsigned long long& nv,
-                                             unsigned long long& nt, unsigned long long& wi, unsigned long long& wl) {
-  h.pos = -1;
-  h.orig = -1;
-  h.t = (D)__builtin_huge_val();
-  h.nan = 0u;
+__device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, LaneTravRows* R, uint32_t lid,
+                                           bool walking, uint32_t yield_lanes, const V& o, const V& d, D time, D tmin,
+                                           WHit& h, unsigned long long& nv, unsigned long long& nt,
+                                           unsigned long long& wi, unsigned long long& wl) {
+  if (!wany(walking)) return false;
+  uint32_t ref = kNoRef, pend = kNoRef, top = kNoRef, sp = 0u;
+  float tmaxf = 0.0f;
+  if (walking) {
+    ref = R->w[0][lid];
+    pend = R->w[1][lid];
+    top = R->w[2][lid];
+    sp = R->w[3][lid];
+    tmaxf = __uint_as_float(R->w[4][lid]);
+    h.pos = (int)R->w[5][lid];
+    h.orig = (int)R->w[6][lid];
+    h.nan = R->w[7][lid];
+    h.t = __builtin_bit_cast(D, (uint64_t)R->w[8][lid] | ((uint64_t)R->w[9][lid] << 32));
+  }
   const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
   const f2 ix = bc((float)inv.x), iy = bc((float)inv.y), iz = bc((float)inv.z);
   const float mf = (float)m;
@@ -467,15 +507,10 @@ __device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack,
   const f2 ozl = bc(pzo - sz * mz), ozh = bc(pzo + sz * mz);
   const float tminf = next_down((float)tmin);
   auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
-  float tmaxf = round_up(h.t);
   const D* pr = W.prim;
   const RaySp ws = ray_space(o, d, W.flags);
-  constexpr uint32_t kNoRef = 0xFFFFFFFFu;  // (never a ref: interior refs < kLeafBit, leaf counts <= 2)
-  // per lane: the node (or leaf) to process next, a postponed leaf, the stack
-  // depth; the stack's top entry lives in a register (`top`, kNoRef when the
-  // stack is empty; entries below it in LDS), so a pop waits on no LDS read:
-  // the next top's read is issued at the pop and lands during the node visit.
-  uint32_t ref = 0u, pend = kNoRef, sp = 0u, top = kNoRef;
+  // the stack's top entry lives in a register (`top`, kNoRef when empty;
+  // entries below it in LDS): a pop waits on no LDS read
   auto pop = [&]() -> uint32_t {
     const uint32_t r = top;
     top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
@@ -485,14 +520,21 @@ __device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack,
     if (top != kNoRef) lstack[(sp++) * 64u + lid] = top;
     top = r;
   };
+  bool yielded = false;
+  // (a phase yields only after some walk finished in it: every phase makes progress)
+  const uint32_t start = popc64(wballot(walking));
   for (;;) {
     // Interior steps.  A lane that reaches a leaf postpones it (one slot) and
-    // keeps traversing; the phase ends once every lane holds a leaf or is out
-    // of work (Aila & Laine's speculative while-while): the leaf tests then
-    // run with most lanes busy.
+    // keeps walking; the phase ends once every lane holds a leaf or is out of
+    // work (speculative while-while): the leaf tests then run with most lanes busy.
     for (;;) {
       const bool step = ref < kLeafBit;
       if (!wany(step & (pend == kNoRef))) break;
+      const uint32_t nact = popc64(wballot((ref != kNoRef) | (pend != kNoRef)));
+      if (nact < yield_lanes && nact < start) {
+        yielded = true;  // few lanes left: pause the walk, let the others take new rays
+        break;
+      }
       if (MODE == 1 && lid == 0) ++wi;
       if (step) {
         if (MODE == 1) ++nv;
@@ -525,6 +567,7 @@ __device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack,
         }
       }
     }
+    if (yielded) break;
     // Leaf tests: the postponed leaf, else a leaf the lane stopped at.
     uint32_t lf = pend;
     if (lf == kNoRef && ref != kNoRef && ref >= kLeafBit) {
@@ -537,18 +580,33 @@ __device__ __forceinline__ void closest_lane(const WV& W, D m, uint32_t* lstack,
       continue;
     }
     if (MODE == 1 && lid == 0) ++wl;
-    static_assert(kMaxLeafPrims <= 2, "closest_lane tests leaves of <= 2 primitives");
-    if (lf != kNoRef) {  // 1 or 2 primitives (kMaxLeafPrims): both records loaded before either test
+    static_assert(kMaxLeafPrims <= 2, "trav_phase tests leaves of <= 2 primitives");
+    if (lf != kNoRef) {  // 1 or 2 primitives (kMaxLeafPrims)
       const uint32_t first = lf & 0x7FFFFFu, cnt = (lf >> 23) & kLeafCountMask;
-      const PrimRec q0 = load_rec(pr + kWorldRec * first);
-      const PrimRec q1 = load_rec(pr + kWorldRec * (cnt > 1u ? first + 1u : first));
-      D t;
-      if (MODE == 1) nt += cnt;
-      if (root_obj<true, FEAT>(q0, ws, time, tmin, t)) accept(h, t, (int)first, (int)q0.orig, tmin);
-      if (cnt > 1u && root_obj<true, FEAT>(q1, ws, time, tmin, t)) accept(h, t, (int)first + 1, (int)q1.orig, tmin);
+      for (uint32_t k = first; k < first + cnt; ++k) {
+        if (MODE == 1) ++nt;
+        D t;
+        const PrimRec q = load_rec(pr + kWorldRec * k);
+        if (root_obj<true, FEAT>(q, ws, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
+      }
       tmaxf = round_up(h.t);
     }
   }
+  const bool finished = walking && ref == kNoRef && pend == kNoRef;
+  if (walking && !finished) {  // paused: keep the walk's state for the next phase
+    R->w[0][lid] = ref;
+    R->w[1][lid] = pend;
+    R->w[2][lid] = top;
+    R->w[3][lid] = sp;
+    R->w[4][lid] = __float_as_uint(tmaxf);
+    R->w[5][lid] = (uint32_t)h.pos;
+    R->w[6][lid] = (uint32_t)h.orig;
+    R->w[7][lid] = h.nan;
+    const uint64_t tb = __builtin_bit_cast(uint64_t, h.t);
+    R->w[8][lid] = (uint32_t)tb;
+    R->w[9][lid] = (uint32_t)(tb >> 32);
+  }
+  return finished;
 }
 
 // Texture.value (texture.zig:36-144) for the winner's record.
@@ -620,7 +678,9 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // this wave's BVH stack: one column per lane (per-lane traversal) or one
   // wave-uniform stack (the union walk)
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) +
-                    (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? kLaneStack * 64u : kBvhStack);
+                    (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? (kLaneStack + kTravWords) * 64u : kBvhStack);
+  // per-lane traversal: this wave's LaneTrav rows follow its stack columns
+  LaneTravRows* trav_rows = reinterpret_cast<LaneTravRows*>(stack + kLaneStack * 64u);
   // Tail dealing rows of this wave's lanes (lane = the owner of a unit): the
   // first sample handed to other lanes (samples [hi, s_end) are theirs), the
   // ring entries they filled, the unit's pixel; and the dealing list.
@@ -671,6 +731,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   LaneFlag<4u> done{lane_flags};
   LaneFlag<8u> waiting{lane_flags};   // owner: its own samples done, waiting for the ones other lanes trace
   LaneFlag<16u> helping{lane_flags};  // helper: traces sample L.s of lane TL_OWN[lid]'s unit
+  LaneFlag<32u> walking{lane_flags};  // per-lane traversal: a paused BVH walk (state in its LaneTrav row)
   uint32_t qnext = 0, qend = 0;
   unsigned long long n_samples = 0, n_segments = 0, n_visits = 0, n_tests = 0, n_iters = 0;
   unsigned long long n_wi = 0, n_wl = 0;  // per-lane traversal: interior / leaf wave iterations
@@ -787,137 +848,157 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     }
     // ---- one segment ----
     bool ended = false;
-    if (have_ray) {
+    // The hit record, texture and scatter of a lane whose closest hit is h
+    // (written once, used by both traversals).
+    auto shade = [&](WHit& h) {
+      if (__builtin_expect(h.nan != 0u, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
+      if (h.pos < 0) {  // miss: background (main.zig:109-112)
+        const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
+        HS(0) += c.x;
+        HS(1) += c.y;
+        HS(2) += c.z;
+        ended = true;
+      } else {
+        // Hit record of the winner (object space, then the wrappers back).
+        const D* r = W.prim + kWorldRec * h.pos;
+        const uint32_t* mt = meta_of(r);
+        const uint32_t kind = mt[0] & 0xFFu;
+        const int xf = (int)(mt[0] >> 8) - 1;
+        V o = L.o, d = L.d;
+        if ((FEAT & kFeatXform) && xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
+        V p = add(o, mul(d, h.t)), nrm;
+        bool front;
+        D tu = 0.0, tv = 0.0;
+        const D* mp = W.mat + 8 * mt[1];
+        const uint32_t* mh = reinterpret_cast<const uint32_t*>(mp);
+        const uint32_t mkind = mh[0], mtex = mh[1];
+        const bool image_tex = (FEAT & kFeatImage) &&
+            (mkind == 0u || mkind == 3u) && *reinterpret_cast<const uint32_t*>(W.tex + kWorldRec * mtex) == 3u;
+        if (!(FEAT & kFeatRect) || kind <= 1u) {
+          V c = ld3(r);
+          if (kind == 1u) c = add(c, mul(ld3(r + 3), (L.time - r[7]) / r[8]));
+          const V outward = divs(sub(p, c), r[6]);
+          front = dot(outward, d) < 0.0;
+          nrm = front ? outward : mul(outward, -1.0);
+          if (kind == 0u && image_tex) {  // getSphereUv (hittable.zig:145-150)
+            const D pi = 3.14159265358979323846;
+            tu = (rtwl::atan2(-outward.z, outward.x) + pi) / (2.0 * pi);
+            tv = rtwl::acos(-outward.y) / pi;
+          }
+        } else {
+          D oa, ob, da, db;
+          V n0;
+          if (kind == 2u) {
+            oa = o.x, ob = o.y, da = d.x, db = d.y, n0 = mk(0.0, 0.0, 1.0);
+          } else if (kind == 3u) {
+            oa = o.x, ob = o.z, da = d.x, db = d.z, n0 = mk(0.0, 1.0, 0.0);
+          } else {
+            oa = o.y, ob = o.z, da = d.y, db = d.z, n0 = mk(1.0, 0.0, 0.0);
+          }
+          tu = (oa + h.t * da - r[0]) / r[5];
+          tv = (ob + h.t * db - r[2]) / r[6];
+          front = dot(n0, d) < 0.0;
+          nrm = front ? n0 : mul(n0, -1.0);
+        }
+        if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
+        if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
+          const V c = mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p));
+          HS(0) += c.x;
+          HS(1) += c.y;
+          HS(2) += c.z;
+          ended = true;
+        } else {
+          V ndir, att;
+          bool absorbed = false;
+          // Lambertian and Metal draw their unit-ball point in ONE per-lane
+          // rejection loop (randomPointInUnitSphere, rand.zig:22-28; the wave
+          // would otherwise run the two loops one after the other), and every
+          // lane makes one normalisation: the ball point (Lambertian) or the
+          // ray direction (Metal, Dielectric).  Same draws, same operations.
+          D b3[3] = {0.0, 0.0, 0.0};
+          if (mkind <= 1u) {
+            for (;;) {
+              b3[0] = rrange_m11<D>(L.rs);
+              b3[1] = rrange_m11<D>(L.rs);
+              b3[2] = rrange_m11<D>(L.rs);
+              if (in_unit_ball<D, 3>(b3)) break;
+            }
+          }
+          const V nv = normalized(mkind == 0u ? mk(b3[0], b3[1], b3[2]) : L.d);
+          if (mkind == 0u) {  // Lambertian (material.zig:44-52)
+            ndir = add(nrm, nv);
+            if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
+            att = tex_value<FEAT>(W, mtex, tu, tv, p);
+          } else {
+            // reflect(ud, nrm) (material.zig:112-114) for Metal and Dielectric;
+            // the Dielectric's dot(-ud, nrm) (:75) is exactly -dun
+            const V& ud = nv;
+            const D dun = dot(ud, nrm);
+            const V refl = sub(ud, mul(nrm, 2 * dun));
+            if (mkind == 1u) {  // Metal (material.zig:59-65)
+              ndir = add(refl, mul(mk(b3[0], b3[1], b3[2]), mp[4]));
+              att = ld3(mp + 1);
+              absorbed = !(dot(refl, nrm) > 0.0);
+            } else {  // Dielectric (material.zig:72-91)
+              const D ir = mp[5];
+              const D ratio = front ? 1.0 / ir : ir;
+              const D cos_t = fmin(-dun, 1.0);
+              const D sin_t = sqrt(1.0 - cos_t * cos_t);
+              bool refr = false;
+              if (ratio * sin_t <= 1.0) {
+                const D r0 = (1.0 - ratio) / (1.0 + ratio);
+                const D r1 = r0 * r0;
+                const D x = 1.0 - cos_t, x2 = x * x;
+                refr = r1 + (1.0 - r1) * (x * (x2 * x2)) < rnd<D>(L.rs);  // Zig pow(x, 5.0)
+              }
+              if (refr) {  // refract (:116-121); its cos_theta is cos_t
+                const V perp = mul(add(ud, mul(nrm, cos_t)), ratio);
+                ndir = add(perp, mul(nrm, -sqrt(fabs(1.0 - norm2(perp)))));
+              } else {
+                ndir = refl;
+              }
+              att = mk(1.0, 1.0, 1.0);
+            }
+          }
+          if (absorbed) {
+            ended = true;
+          } else {
+            L.T = mulv(L.T, att);
+            L.o = p;
+            L.d = ndir;
+            L.depth++;
+          }
+        }
+      }
+    };
+    if constexpr ((FEAT & kFeatLane) != 0) {
+      if (have_ray && !walking) {
+        if (L.depth == WKA(t.max_depth)) {
+          ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
+        } else {
+          walking = true;
+          trav_begin(trav_rows, lid);
+          if (MODE == 1) ++n_segments;
+        }
+      }
+      WSTAMP(1)  // sample start (+ take units, loop control)
+      // once every lane's unit queue ran dry, walks run to their end (no yield)
+      const uint32_t yl = wall(done) ? 0u : WKA(lane_yield);
+      WHit h;
+      if (trav_phase<MODE, FEAT>(W, WKA(margin), stack, trav_rows, lid, walking, yl, L.o, L.d, L.time, WKA(t.tmin),
+                                 h, n_visits, n_tests, n_wi, n_wl)) {
+        walking = false;
+        shade(h);
+      }
+    } else if (have_ray) {
       if (L.depth == WKA(t.max_depth)) {
         ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
       } else {
         if (MODE == 1) ++n_segments;
         WHit h;
         WSTAMP(1)  // sample start (+ take units, loop control)
-        if constexpr ((FEAT & kFeatLane) != 0)
-          closest_lane<MODE, FEAT>(W, WKA(margin), stack, lid, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests,
-                                   n_wi, n_wl);
-        else
-          closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
-        if (__builtin_expect(h.nan != 0u, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
-        if (h.pos < 0) {  // miss: background (main.zig:109-112)
-          const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
-          HS(0) += c.x;
-          HS(1) += c.y;
-          HS(2) += c.z;
-          ended = true;
-        } else {
-          // Hit record of the winner (object space, then the wrappers back).
-          const D* r = W.prim + kWorldRec * h.pos;
-          const uint32_t* mt = meta_of(r);
-          const uint32_t kind = mt[0] & 0xFFu;
-          const int xf = (int)(mt[0] >> 8) - 1;
-          V o = L.o, d = L.d;
-          if ((FEAT & kFeatXform) && xf >= 0) to_object(W.xform + kWorldRec * xf, o, d);
-          V p = add(o, mul(d, h.t)), nrm;
-          bool front;
-          D tu = 0.0, tv = 0.0;
-          const D* mp = W.mat + 8 * mt[1];
-          const uint32_t* mh = reinterpret_cast<const uint32_t*>(mp);
-          const uint32_t mkind = mh[0], mtex = mh[1];
-          const bool image_tex = (FEAT & kFeatImage) &&
-              (mkind == 0u || mkind == 3u) && *reinterpret_cast<const uint32_t*>(W.tex + kWorldRec * mtex) == 3u;
-          if (!(FEAT & kFeatRect) || kind <= 1u) {
-            V c = ld3(r);
-            if (kind == 1u) c = add(c, mul(ld3(r + 3), (L.time - r[7]) / r[8]));
-            const V outward = divs(sub(p, c), r[6]);
-            front = dot(outward, d) < 0.0;
-            nrm = front ? outward : mul(outward, -1.0);
-            if (kind == 0u && image_tex) {  // getSphereUv (hittable.zig:145-150)
-              const D pi = 3.14159265358979323846;
-              tu = (rtwl::atan2(-outward.z, outward.x) + pi) / (2.0 * pi);
-              tv = rtwl::acos(-outward.y) / pi;
-            }
-          } else {
-            D oa, ob, da, db;
-            V n0;
-            if (kind == 2u) {
-              oa = o.x, ob = o.y, da = d.x, db = d.y, n0 = mk(0.0, 0.0, 1.0);
-            } else if (kind == 3u) {
-              oa = o.x, ob = o.z, da = d.x, db = d.z, n0 = mk(0.0, 1.0, 0.0);
-            } else {
-              oa = o.y, ob = o.z, da = d.y, db = d.z, n0 = mk(1.0, 0.0, 0.0);
-            }
-            tu = (oa + h.t * da - r[0]) / r[5];
-            tv = (ob + h.t * db - r[2]) / r[6];
-            front = dot(n0, d) < 0.0;
-            nrm = front ? n0 : mul(n0, -1.0);
-          }
-          if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
-          if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
-            const V c = mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p));
-            HS(0) += c.x;
-            HS(1) += c.y;
-            HS(2) += c.z;
-            ended = true;
-          } else {
-            V ndir, att;
-            bool absorbed = false;
-            // Lambertian and Metal draw their unit-ball point in ONE per-lane
-            // rejection loop (randomPointInUnitSphere, rand.zig:22-28; the wave
-            // would otherwise run the two loops one after the other), and every
-            // lane makes one normalisation: the ball point (Lambertian) or the
-            // ray direction (Metal, Dielectric).  Same draws, same operations.
-            D b3[3] = {0.0, 0.0, 0.0};
-            if (mkind <= 1u) {
-              for (;;) {
-                b3[0] = rrange_m11<D>(L.rs);
-                b3[1] = rrange_m11<D>(L.rs);
-                b3[2] = rrange_m11<D>(L.rs);
-                if (in_unit_ball<D, 3>(b3)) break;
-              }
-            }
-            const V nv = normalized(mkind == 0u ? mk(b3[0], b3[1], b3[2]) : L.d);
-            if (mkind == 0u) {  // Lambertian (material.zig:44-52)
-              ndir = add(nrm, nv);
-              if (fabs(ndir.x) < 1e-8 && fabs(ndir.y) < 1e-8 && fabs(ndir.z) < 1e-8) ndir = nrm;
-              att = tex_value<FEAT>(W, mtex, tu, tv, p);
-            } else {
-              // reflect(ud, nrm) (material.zig:112-114) for Metal and Dielectric;
-              // the Dielectric's dot(-ud, nrm) (:75) is exactly -dun
-              const V& ud = nv;
-              const D dun = dot(ud, nrm);
-              const V refl = sub(ud, mul(nrm, 2 * dun));
-              if (mkind == 1u) {  // Metal (material.zig:59-65)
-                ndir = add(refl, mul(mk(b3[0], b3[1], b3[2]), mp[4]));
-                att = ld3(mp + 1);
-                absorbed = !(dot(refl, nrm) > 0.0);
-              } else {  // Dielectric (material.zig:72-91)
-                const D ir = mp[5];
-                const D ratio = front ? 1.0 / ir : ir;
-                const D cos_t = fmin(-dun, 1.0);
-                const D sin_t = sqrt(1.0 - cos_t * cos_t);
-                bool refr = false;
-                if (ratio * sin_t <= 1.0) {
-                  const D r0 = (1.0 - ratio) / (1.0 + ratio);
-                  const D r1 = r0 * r0;
-                  const D x = 1.0 - cos_t, x2 = x * x;
-                  refr = r1 + (1.0 - r1) * (x * (x2 * x2)) < rnd<D>(L.rs);  // Zig pow(x, 5.0)
-                }
-                if (refr) {  // refract (:116-121); its cos_theta is cos_t
-                  const V perp = mul(add(ud, mul(nrm, cos_t)), ratio);
-                  ndir = add(perp, mul(nrm, -sqrt(fabs(1.0 - norm2(perp)))));
-                } else {
-                  ndir = refl;
-                }
-                att = mk(1.0, 1.0, 1.0);
-              }
-            }
-            if (absorbed) {
-              ended = true;
-            } else {
-              L.T = mulv(L.T, att);
-              L.o = p;
-              L.d = ndir;
-              L.depth++;
-            }
-          }
-        }
+        closest<MODE, FEAT>(W, WKA(margin), stack, L.o, L.d, L.time, WKA(t.tmin), h, n_visits, n_tests, st);
+        shade(h);
       }
     }
     WSTAMP(4)  // hit record, texture, scatter (+ the NaN fallback)
@@ -1013,7 +1094,8 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 }
 
 size_t world_lds_bytes(uint32_t, int fs) {
-  return (size_t)((fs & kFeatLane) ? kLaneStack * 64u : kBvhStack) * (kWorldBlock / 64) * sizeof(uint32_t);
+  return (size_t)((fs & kFeatLane) ? (kLaneStack + kTravWords) * 64u : kBvhStack) * (kWorldBlock / 64) *
+         sizeof(uint32_t);
 }
 
 template <int OCC, int FEAT>

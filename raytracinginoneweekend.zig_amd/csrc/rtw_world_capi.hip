@@ -574,6 +574,7 @@ struct WorldLaunchCfg {
   uint32_t grid;
   size_t ring_off, ring_bytes;  // ring: [ring_off, ring_off + ring_bytes) of the workspace
 };
+constexpr uint32_t kLaneYield = 24;  // (tools/world_bench.py A/B of RTW_WORLD_YIELD)
 WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   WorldLaunchCfg c;
   // Kernel instantiation for the world's features (params.world_features
@@ -640,6 +641,10 @@ int world_launch(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* 
   const char* te = rtw_dev_knob("RTW_WORLD_TAIL");
   a.tail_deal = ((te && *te == '0') || ws_bytes < c.ring_off + c.ring_bytes) ? 0u : 1u;
   a.ring = a.tail_deal ? reinterpret_cast<double*>(wsb + c.ring_off) : nullptr;
+  // per-lane traversal: pause a wave's walks once fewer than this many lanes
+  // still walk (development knob RTW_WORLD_YIELD)
+  const char* ye = rtw_dev_knob("RTW_WORLD_YIELD");
+  a.lane_yield = (ye && *ye) ? (uint32_t)atoi(ye) : kLaneYield;
   if (tail_ran) *tail_ran = a.tail_deal;
   const size_t lds = c.lds;
   const uint32_t grid = c.grid;

@@ -119,3 +119,22 @@ def test_design_traffic_figures_are_the_committed_json():
         scale = 1e6 if unit == "MB" else 1e9
         digits = len(val.split(".")[1]) if "." in val else 0
         assert abs(float(val) - b / scale) <= 0.5 * 10 ** -digits + 1e-12, (name, val, unit, b)
+
+
+def test_design_has_no_unfilled_template_tokens():
+    """DESIGN.md once carried unfilled placeholders
+    (`PORT_BOX`, `TIERA_BOX`).  Upper-case snake tokens of that shape that are
+    not identifiers of this repository (RTW_* macros and env names, rtw_hip.h
+    constants, file names) must not appear."""
+    import re
+    txt = open(os.path.join(REPO, "DESIGN.md")).read()
+    known = set(re.findall(r"\b[A-Z][A-Z0-9]*(?:_[A-Z0-9]+)+\b", open(os.path.join(REPO, "include", "rtw_hip.h")).read()))
+    bad = []
+    for tok in set(re.findall(r"\b[A-Z][A-Z0-9]*(?:_[A-Z0-9]+)+\b", txt)):
+        if tok.startswith(("RTW_", "DRTW_", "DBL_", "FLT_", "SQ_", "TCC_", "TCP_", "GRBM_", "HSA_", "GPU_", "HIP_",
+                           "OMP_", "MAX_")) or tok in known:
+            continue
+        if tok in ("FETCH_SIZE", "WRITE_SIZE", "VAR_BIT", "TIER_A", "TIER_B") or tok.endswith(("_MHZ", "_MS")):
+            continue
+        bad.append(tok)
+    assert not bad, sorted(bad)
