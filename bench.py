@@ -61,6 +61,7 @@ def parse_args(argv=None):
     ap.add_argument("--wf-sets", type=int, default=0, help="wavefront queue sets, params.wf_sets (0 = library default)")
     ap.add_argument("--wf-drain", default="samples", choices=["samples", "slots", "none"], help="params.wf_drain")
     ap.add_argument("--wf-form", default="fused", choices=["fused", "split"], help="params.wf_form")
+    ap.add_argument("--wf-bounces", type=int, default=0, help="params.wf_bounces: bounce segments per wf_step launch")
     ap.add_argument("--no-wavefront-variant", action="store_true")
     ap.add_argument("--no-world-variants", action="store_true", help="skip the configs[4] globe and Cornell lines")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2],
@@ -170,7 +171,8 @@ def wf_sets(args):
 
 def wf_params(args):
     """The wavefront engine's configuration fields of rtw_params (ABI v4)."""
-    return dict(wf_paths=args.wf_paths, wf_sets=args.wf_sets, wf_drain=args.wf_drain, wf_form=args.wf_form)
+    return dict(wf_paths=args.wf_paths, wf_sets=args.wf_sets, wf_drain=args.wf_drain, wf_form=args.wf_form,
+                wf_bounces=args.wf_bounces)
 
 
 def wf_kernels(args):
@@ -365,7 +367,7 @@ def world_variant(R, torch, scene, steps, warmup):
             "note": "world kernel, f64, bit-identical to oracle Tier B (tests/test_gpu_world.py)"}
 
 
-def wavefront_bytes(counts, precision, units, fused=True):
+def wavefront_bytes(counts, precision, units, fused=True, bounces=1):
     """Algorithmic HBM bytes of one wavefront frame (rtw_wavefront.hip): per
     bounce segment of the fused engine (default), wf_step reads the path +
     its hit (root, winner) and writes the next path + its hit; of the split
@@ -375,7 +377,9 @@ def wavefront_bytes(counts, precision, units, fused=True):
     (read + write).  Per unit: the f64x3 chunk sum.  `counts` is the
     wavefront engine's own counts pass: segments traced by the in-register
     drain (wf_finish, counts["drain_segments"]) move no queue bytes (its one
-    load of each live path, <= 96 B x slots, is left out: < 0.1 %)."""
+    load of each live path, <= 96 B x slots, is left out: < 0.1 %).  With
+    `bounces` segments per wf_step launch (params.wf_bounces) a path crosses
+    the queues once per `bounces` segments."""
     r = 8 if precision == "f64" else 4
     path = 10 * r + 8 + 4 + 4
     if fused:  # fused engine: path + hit read, path + hit written
@@ -383,7 +387,7 @@ def wavefront_bytes(counts, precision, units, fused=True):
     else:  # extend reads o, d, time (+ skip), writes the hit; shade reads path + hit, writes the path
         seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
     queued = counts["segments"] - counts.get("drain_segments", 0)
-    return queued * seg + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
+    return queued * seg // max(1, bounces) + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
 
 
 def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, samples_all, world, rank, dist,
@@ -419,12 +423,47 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     sclk = clk.mhz()
     chunk = min(R.DEFAULT_CHUNK, spp)
     units = rc * W * ((spp + chunk - 1) // chunk)
-    byts = wavefront_bytes(counts, args.precision, units, args.wf_form == "fused")
+    kb = args.wf_bounces or 1
+    byts = wavefront_bytes(counts, args.precision, units, args.wf_form == "fused", kb if args.wf_form == "fused" else 1)
     gbs = byts / (ms * 1e-3) / 1e9
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
+    # The same frame with 2 and 3 bounce segments per wf_step launch
+    # (params.wf_bounces; the path kept in registers between them: fewer,
+    # longer launches and 1/K of the queue bytes), timed the same way.
+    sweep = {}
+    if args.wf_bounces == 0 and args.wf_form == "fused":
+        for k in (2, 3):
+            pk = R.make_params(W, H, spp, DEPTH, SEED, row_begin=rb, row_stride=rs, row_count=rc,
+                               precision=args.precision, engine="wavefront", **{**wf_params(args), "wf_bounces": k})
+            warm(lambda: rend.render(cam, pk, out=out), 1, torch)
+            tk = [R.Timer() for _ in range(args.steps)]
+            if world > 1:
+                dist.barrier()
+            a = time.perf_counter()
+            for i in range(args.steps):
+                rend.render(cam, pk, out=out, timer=tk[i])
+                if world > 1:
+                    tg.gather(out)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ek = time.perf_counter() - a
+            if world > 1:
+                t = torch.tensor([ek], dtype=torch.float64, device=out.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                ek = float(t.item())
+            msk = sum(t.elapsed_ms() for t in tk) / len(tk)
+            for t in tk:
+                t.close()
+            bk = wavefront_bytes(counts, args.precision, units, True, k)
+            sweep[str(k)] = {"value": round(samples_all * args.steps / ek / 1e6, 2),
+                             "ms_per_step": round(ek / args.steps * 1e3, 3), "loop_ms_per_frame": round(msk, 3),
+                             "hbm_frac": round(bk / (msk * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                             "algorithmic_bytes_per_frame": bk}
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
-            "wf_form": args.wf_form, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
+            "wf_form": args.wf_form, "wf_bounces": kb, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
+            "bounces_per_launch": sweep,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),
                          "traffic_source": os.path.relpath(evidence("wf_traffic.json"), REPO),

@@ -102,7 +102,7 @@ typedef enum {
   RTW_WORLD_FEATURES_ALL = 1   /* the general kernel (every primitive, texture and transform) */
 } rtw_world_features;
 typedef enum {
-  RTW_WORLD_TRAVERSAL_AUTO = 0,  /* the default for the world */
+  RTW_WORLD_TRAVERSAL_AUTO = 0,  /* per lane for sphere worlds of >= 256 BVH nodes, else the union */
   RTW_WORLD_TRAVERSAL_UNION = 1, /* the wave walks the union of its lanes' BVH paths (scalar node loads) */
   RTW_WORLD_TRAVERSAL_LANE = 2   /* every lane walks its own path (sphere worlds with a BVH of depth <= 24;
                                     other worlds take the union walk) */
@@ -132,6 +132,9 @@ typedef struct {
                                  0 = the feature set's default (4 sphere worlds, 3 rects / transforms, 2 noise) */
   uint32_t world_features;    /* world kernel: rtw_world_features */
   uint32_t world_traversal;   /* world kernel: rtw_world_traversal */
+  uint32_t wf_bounces;        /* wavefront: bounce segments per path per wf_step launch (the path stays in
+                                 registers between them), 0 = 1: one queue exchange per bounce (configs[3]) */
+  uint32_t reserved;          /* must be 0 */
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u

@@ -517,6 +517,8 @@ int validate(const rtw_params* p) {
   if (p->world_waves > 4) return fail(RTW_EINVAL, "world_waves %u outside [0, 4]", p->world_waves);
   if (p->world_features > RTW_WORLD_FEATURES_ALL) return fail(RTW_EINVAL, "world_features %u", p->world_features);
   if (p->world_traversal > RTW_WORLD_TRAVERSAL_LANE) return fail(RTW_EINVAL, "world_traversal %u", p->world_traversal);
+  if (p->wf_bounces > 16) return fail(RTW_EINVAL, "wf_bounces %u outside [0, 16]", p->wf_bounces);
+  if (p->reserved != 0) return fail(RTW_EINVAL, "params.reserved must be 0");
   if (p->engine == RTW_ENGINE_WAVEFRONT && (p->wf_paths > (1u << 28) || (p->wf_paths && p->wf_paths < 64)))
     return fail(RTW_EINVAL, "wf_paths %u outside [64, 2^28]", p->wf_paths);
   if (p->engine == RTW_ENGINE_WAVEFRONT && p->max_depth > 0xFFFFu)
@@ -798,7 +800,6 @@ struct WfSet {
 // launches: every wave reads its count first.  Sets run on their own streams,
 // forked from and joined back to the caller's stream.
 constexpr uint32_t kWfBatch = 64;
-constexpr uint32_t kWfBounces = 1;
 constexpr int kWfIters = 8;  // even: each batch ends with the live paths in queue A
 template <typename R>
 int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned char* ws, const WsLayout& L, int dev,
@@ -815,10 +816,9 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // runs dry.
   const char* be = dev_knob("RTW_WF_BATCH");
   const uint32_t refill = (be && *be) ? (uint32_t)std::max(1, atoi(be)) : kWfBatch;
-  // Bounce segments per path per wf_step launch (kWfBounces; development knob
-  // RTW_WF_BOUNCES): the path stays in registers between them.
-  const char* bo = dev_knob("RTW_WF_BOUNCES");
-  const uint32_t bounces = (bo && *bo) ? (uint32_t)std::max(1, atoi(bo)) : kWfBounces;
+  // Bounce segments per path per wf_step launch (params.wf_bounces, 0 = 1):
+  // the path stays in registers between them.
+  const uint32_t bounces = p->wf_bounces ? p->wf_bounces : 1u;
   // Persistent grids: every resident wave slot of each bounce kernel (at most
   // one wave per segment); the same grids for every launch of the frame.
   // The drains always run max_grid = ceil(segs / waves per block) blocks: one

@@ -574,7 +574,8 @@ struct WorldLaunchCfg {
   uint32_t grid;
   size_t ring_off, ring_bytes;  // ring: [ring_off, ring_off + ring_bytes) of the workspace
 };
-constexpr uint32_t kLaneYield = 24;  // (tools/world_bench.py A/B of RTW_WORLD_YIELD)
+constexpr uint32_t kLaneYield = 24;   // (tools/world_bench.py A/B of RTW_WORLD_YIELD)
+constexpr uint32_t kLaneNodes = 256;  // AUTO traversal: per lane from this BVH size on
 WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   WorldLaunchCfg c;
   // Kernel instantiation for the world's features (params.world_features
@@ -582,8 +583,12 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   // and its BVH traversal (params.world_traversal): per lane for sphere worlds
   // whose BVH fits the per-lane stack, else the wave's union walk.
   const uint32_t feat = p->world_features == RTW_WORLD_FEATURES_ALL ? 15u : w->feat;
-  const bool lane = p->world_traversal == RTW_WORLD_TRAVERSAL_LANE && w->view.n_nodes > 0 &&
-                    w->info[2] <= rtwk::kLaneStack && w->info[3] <= 2u;
+  // AUTO: per lane on BVHs of >= kLaneNodes nodes (configs[4]'s globe: 5,802
+  // nodes, +30 %); the union walk on small trees, where the lanes' paths
+  // mostly coincide (scene 1's 23 nodes: the union 17 % faster).
+  const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= 2u;
+  const bool lane = lane_ok && (p->world_traversal == RTW_WORLD_TRAVERSAL_LANE ||
+                                (p->world_traversal == RTW_WORLD_TRAVERSAL_AUTO && w->view.n_nodes >= kLaneNodes));
   c.fs = rtwk::world_feature_set(feat, lane);
   c.lds = rtwk::world_lds_bytes(w->view.n_perlins, c.fs);
   // Register-allocation target in waves per SIMD (params.world_waves, 0 = the

@@ -71,7 +71,8 @@ class Params(C.Structure):
                 ("chunk", C.c_uint32), ("precision", C.c_uint32), ("device", C.c_int32),
                 ("engine", C.c_uint32), ("wf_paths", C.c_uint32),
                 ("wf_sets", C.c_uint32), ("wf_drain", C.c_uint32), ("wf_form", C.c_uint32),
-                ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("world_traversal", C.c_uint32)]
+                ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("world_traversal", C.c_uint32),
+                ("wf_bounces", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 _lib = None
@@ -178,7 +179,7 @@ def cover_scene(seed: int = 42):
 def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACKGROUND, row_begin=0,
                 row_stride=1, row_count=None, chunk=0, precision="f64", device=-1, engine="megakernel",
                 wf_paths=0, wf_sets=0, wf_drain="samples", wf_form="fused", world_waves=0,
-                world_features="auto", world_traversal="auto") -> Params:
+                world_features="auto", world_traversal="auto", wf_bounces=0) -> Params:
     """rtw_params (ABI v4): every engine choice is a field (0 / the first
     name = the library default); nothing is read from the environment."""
     if row_count is None:
@@ -191,7 +192,7 @@ def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACK
     return Params(width, height, spp, max_depth, seed, (C.c_double * 3)(*background), row_begin, row_stride,
                   row_count, chunk, prec, device, eng, wf_paths, wf_sets, enum(wf_drain, WF_DRAIN),
                   enum(wf_form, WF_FORM), world_waves, enum(world_features, WORLD_FEATURES),
-                  enum(world_traversal, WORLD_TRAVERSAL))
+                  enum(world_traversal, WORLD_TRAVERSAL), wf_bounces, 0)
 
 
 def _arr(x, typ):

@@ -27,7 +27,7 @@ def test_struct_layouts_match_header(rtw):
     assert C.sizeof(rtw.Material) == 8 + 3 * 8 * 2 + 16
     assert C.sizeof(rtw.Sphere) == 6 * 8 + 3 * 8 + 8
     assert C.sizeof(rtw.Camera) == 7 * 24 + 24
-    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12 + 8 + 6 * 4  # + ABI v4 engine fields
+    assert C.sizeof(rtw.Params) == 16 + 8 + 24 + 12 + 12 + 8 + 8 * 4  # + ABI v4 engine fields
 
 
 def test_cover_scene_equals_oracle_golden(rtw):
@@ -189,7 +189,8 @@ def test_product_library_reads_no_environment():
 
 
 @pytest.mark.parametrize("field,value", [("wf_sets", 5), ("wf_drain", 3), ("wf_form", 2), ("world_waves", 5),
-                                         ("world_features", 2), ("world_traversal", 3)])
+                                         ("world_features", 2), ("world_traversal", 3), ("wf_bounces", 17),
+                                         ("reserved", 1)])
 def test_params_v4_fields_validated(rtw, field, value):
     p = rtw.make_params(64, 36, 1, engine="wavefront")
     setattr(p, field, value)

@@ -134,11 +134,13 @@ def test_wavefront_row_shards(rtw, cover):
             assert (part == full[r::world]).all(), (world, r)
 
 
+@pytest.mark.parametrize("bounces", [1, 3])
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
+def test_wavefront_config2_full_frame_identical(rtw, cover, precision, bounces):
     """configs[1] at full size (1200x675x500): the wavefront frame equals the
     megakernel frame byte for byte (the megakernel's rows are oracle-checked
-    in test_gpu_parity.py)."""
+    in test_gpu_parity.py) — with one bounce segment per wf_step launch and
+    with three (params.wf_bounces: the path kept in registers between them)."""
     import torch
     from rtw_amd.device import TorchRenderer
 
@@ -146,7 +148,7 @@ def test_wavefront_config2_full_frame_identical(rtw, cover, precision):
     R = TorchRenderer(sph, mats, 0)
     outs = []
     for eng in ("megakernel", "wavefront"):
-        p = rtw.make_params(1200, 675, 500, precision=precision, engine=eng)
+        p = rtw.make_params(1200, 675, 500, precision=precision, engine=eng, wf_bounces=bounces)
         rgb = torch.empty((675, 1200, 3), dtype=torch.uint8, device="cuda:0")
         mean = torch.empty((675, 1200, 3), dtype=torch.float32, device="cuda:0")
         R.render(cam, p, out=rgb, mean=mean)
