@@ -507,7 +507,14 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
   const f2 ozl = bc(pzo - sz * mz), ozh = bc(pzo + sz * mz);
   const float tminf = next_down((float)tmin);
   auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
-  const D* pr = W.prim;
+  // the node and primitive tables' addresses, read from the kernel argument
+  // once per phase (re-read in the loop, the scalar load's lgkmcnt wait also
+  // waited for the stack pop's LDS read, which `top` is there to hide)
+  using GF = const __attribute__((address_space(1))) float;  // global: vector memory loads, not flat
+  GF* nodes = (GF*)W.node;
+  using GD = const __attribute__((address_space(1))) D;
+  GD* pr = (GD*)W.prim;
+  asm volatile("" : "+s"(nodes), "+s"(pr));
   const RaySp ws = ray_space(o, d, W.flags);
   // the stack's top entry lives in a register (`top`, kNoRef when empty;
   // entries below it in LDS): a pop waits on no LDS read
@@ -538,8 +545,11 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
       if (MODE == 1 && lid == 0) ++wi;
       if (step) {
         if (MODE == 1) ++nv;
-        const float4* nd = reinterpret_cast<const float4*>(W.node + (size_t)ref * kNodeWords);
-        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        // (a 32-bit byte offset from the SGPR base: the loads' saddr form, no 64-bit address math)
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
+            reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 6));
+        const f4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
         // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3, refs in words 12-13
         const f2 x0 = pfma(f2{q0.x, q0.y}, ix, oxl), x1 = pfma(f2{q1.z, q1.w}, ix, oxh);
         const f2 y0 = pfma(f2{q0.z, q0.w}, iy, oyl), y1 = pfma(f2{q2.x, q2.y}, iy, oyh);
@@ -582,11 +592,13 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     if (MODE == 1 && lid == 0) ++wl;
     static_assert(kMaxLeafPrims <= 2, "trav_phase tests leaves of <= 2 primitives");
     if (lf != kNoRef) {  // 1 or 2 primitives (kMaxLeafPrims)
+      static_assert(kWorldRec * sizeof(D) == 128, "primitive record size");
       const uint32_t first = lf & 0x7FFFFFu, cnt = (lf >> 23) & kLeafCountMask;
       for (uint32_t k = first; k < first + cnt; ++k) {
         if (MODE == 1) ++nt;
         D t;
-        const PrimRec q = load_rec(pr + kWorldRec * k);
+        const PrimRec q = load_rec(reinterpret_cast<GD*>(reinterpret_cast<const __attribute__((address_space(1))) char*>(pr) +
+                                                         (k << 7)));  // (kWorldRec doubles = 128 B)
         if (root_obj<true, FEAT>(q, ws, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
       }
       tmaxf = round_up(h.t);

@@ -574,7 +574,7 @@ struct WorldLaunchCfg {
   uint32_t grid;
   size_t ring_off, ring_bytes;  // ring: [ring_off, ring_off + ring_bytes) of the workspace
 };
-constexpr uint32_t kLaneYield = 24;   // (tools/world_bench.py A/B of RTW_WORLD_YIELD)
+constexpr uint32_t kLaneYield = 16;   // (A/B of RTW_WORLD_YIELD 12 / 16 / 24 / 32: profiles/r05/world_lane_ab.txt)
 constexpr uint32_t kLaneNodes = 256;  // AUTO traversal: per lane from this BVH size on
 WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   WorldLaunchCfg c;
