@@ -262,17 +262,21 @@ def cpu_baseline(width, height, spp_sample):
     return res
 
 
-def world_roofline(scene, s, kernel_ms, info):
-    """Roofline of the world kernel: VALU issue.  Its records are wave-uniform
-    scalar loads (no per-lane byte stream to price against HBM), so the roof
-    is the SIMDs' instruction issue: 1024 SIMDs x clock / 4 cycles per wave64
-    VALU instruction.  achieved = the VALU instructions of one launch (PMC
-    SQ_INSTS_VALU of the same config, profiles/rNN/world_pmc_<scene>.json,
+def world_roofline(scene, s, kernel_ms, info, lane=False):
+    """Roofline of the world kernel: VALU issue.  Its byte stream is tiny
+    (records and BVH nodes are L2-resident: nothing to price against HBM), so
+    the roof is the SIMDs' instruction issue: 1024 SIMDs x clock / 4 cycles per
+    wave64 VALU instruction.  achieved = the VALU instructions of one launch
+    (PMC SQ_INSTS_VALU of the same config, profiles/rNN/world_pmc_<scene>.json,
     tools/gpu_world_pmc.sh + tools/world_pmc_json.py) / the launch time
-    measured here; traffic = its PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE."""
+    measured here; traffic = its PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE.
+    With the per-lane BVH walk (lane) the instructions are each lane's own
+    path, not the union of the wave's: the line's node visits per segment are
+    per lane (the algorithm's work), and wait_frac shows the remaining bound,
+    the dependent per-lane node loads."""
     path = evidence(f"world_pmc_{scene}.json")
-    bound = ("valu-issue (wave-uniform scalar-loaded records" +
-             ("; wave-cooperative BVH traversal)" if info["nodes"] else "; linear list, no BVH)"))
+    trav = "per-lane BVH walks (vector node loads)" if lane else "wave-cooperative BVH traversal (scalar node loads)"
+    bound = "valu-issue (" + (trav if info["nodes"] else "wave-uniform scalar-loaded records; linear list, no BVH") + ")"
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
@@ -354,10 +358,12 @@ def world_variant(R, torch, scene, steps, warmup):
     info = dw.bvh_info()
     dw.close()
     samples = s.width * s.height * s.spp
-    roof = world_roofline(scene, s, ms, info)
+    lane = c.get("lane_interior_iters", 0) > 0
+    roof = world_roofline(scene, s, ms, info, lane)
     return {"value": round(samples * steps / e / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(e / steps * 1e3, 3),
             "kernel_ms": round(ms, 3), "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
             "tail_dealing": c["tail_dealing"],
+            "traversal": ("per-lane walks" if lane else "wave union") if info["nodes"] else "linear",
             "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
                                                   "height": s.height, "spp": s.spp, "max_depth": DEPTH},
             "bvh": info, "segments_per_sample": round(c["segments"] / samples, 3),
