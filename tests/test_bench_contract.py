@@ -11,7 +11,7 @@ import os
 
 from conftest import REPO
 
-ROUND = "r04"
+ROUND = "r05"
 BENCH = os.path.join(REPO, "profiles", ROUND, "bench.json")
 
 
