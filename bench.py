@@ -62,6 +62,7 @@ def parse_args(argv=None):
     ap.add_argument("--wf-drain", default="samples", choices=["samples", "slots", "none"], help="params.wf_drain")
     ap.add_argument("--wf-form", default="fused", choices=["fused", "split"], help="params.wf_form")
     ap.add_argument("--wf-bounces", type=int, default=0, help="params.wf_bounces: bounce segments per wf_step launch")
+    ap.add_argument("--wf-passes", type=int, default=0, help="params.wf_passes: queue passes per wf_step launch")
     ap.add_argument("--no-wavefront-variant", action="store_true")
     ap.add_argument("--no-world-variants", action="store_true", help="skip the configs[4] globe and Cornell lines")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2],
@@ -158,7 +159,8 @@ def wf_traffic(args, W, rc, spp):
     c = t.get("config", {})
     fused = args.wf_form == "fused"
     if not same_per_rank_work(c, args, W, rc, spp) or args.wf_paths != 0 or c.get("fused", False) != fused \
-            or c.get("sets", 1) != wf_sets(args) or args.wf_drain != "samples":
+            or c.get("sets", 1) != wf_sets(args) or args.wf_drain != "samples" \
+            or (fused and c.get("passes", 1) != wf_passes(args)) or (args.wf_bounces or 1) != c.get("bounces", 1):
         return None
     return round(t["traffic_bytes_per_frame"])
 
@@ -169,10 +171,16 @@ def wf_sets(args):
     return int(args.wf_sets or R.DEFAULT_WF_SETS)
 
 
+def wf_passes(args):
+    """Queue passes per wf_step launch (--wf-passes = params.wf_passes, else the library default)."""
+    import rtw_amd as R
+    return int(args.wf_passes or R.DEFAULT_WF_PASSES)
+
+
 def wf_params(args):
     """The wavefront engine's configuration fields of rtw_params (ABI v4)."""
     return dict(wf_paths=args.wf_paths, wf_sets=args.wf_sets, wf_drain=args.wf_drain, wf_form=args.wf_form,
-                wf_bounces=args.wf_bounces)
+                wf_bounces=args.wf_bounces, wf_passes=args.wf_passes)
 
 
 def wf_kernels(args):
@@ -468,7 +476,8 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
                              "algorithmic_bytes_per_frame": bk}
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
-            "wf_form": args.wf_form, "wf_bounces": kb, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
+            "wf_form": args.wf_form, "wf_bounces": kb,
+            "wf_passes": wf_passes(args) if args.wf_form == "fused" else 1, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
             "bounces_per_launch": sweep,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),

@@ -518,7 +518,7 @@ int validate(const rtw_params* p) {
   if (p->world_features > RTW_WORLD_FEATURES_ALL) return fail(RTW_EINVAL, "world_features %u", p->world_features);
   if (p->world_traversal > RTW_WORLD_TRAVERSAL_LANE) return fail(RTW_EINVAL, "world_traversal %u", p->world_traversal);
   if (p->wf_bounces > 16) return fail(RTW_EINVAL, "wf_bounces %u outside [0, 16]", p->wf_bounces);
-  if (p->reserved != 0) return fail(RTW_EINVAL, "params.reserved must be 0");
+  if (p->wf_passes > 64) return fail(RTW_EINVAL, "wf_passes %u outside [0, 64]", p->wf_passes);
   if (p->engine == RTW_ENGINE_WAVEFRONT && (p->wf_paths > (1u << 28) || (p->wf_paths && p->wf_paths < 64)))
     return fail(RTW_EINVAL, "wf_paths %u outside [64, 2^28]", p->wf_paths);
   if (p->engine == RTW_ENGINE_WAVEFRONT && p->max_depth > 0xFFFFu)
@@ -839,6 +839,10 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   // shade kernels): one kernel per bounce, the closest hit computed where the
   // ray is made.
   const bool fused = p->wf_form == RTW_WF_FUSED;
+  // Queue passes per wf_step launch (params.wf_passes, fused form): each pass
+  // moves every path through the queues; a batch holds >= kWfIters passes.
+  const uint32_t passes = !fused ? 1u : p->wf_passes ? p->wf_passes : RTW_DEFAULT_WF_PASSES;
+  const int iters = std::max(2, (kWfIters / (int)passes) & ~1);  // even: the batch ends with the paths in queue A
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
   WfSet<R> set[kWfMaxSets];
@@ -871,6 +875,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     a.n_segs = segs;
     a.batch = refill;
     a.bounces = bounces;
+    a.passes = passes;
     S.s = k == 0 ? stream : wf_side_stream(dev, k);  // (set 0: the caller's stream, NULL = the default stream)
     if (k > 0 && !S.s) {
       st = fail(RTW_EHIP, "wavefront side stream creation failed");
@@ -892,7 +897,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   }
   // Termination bound (never reached by a correct kernel): every iteration
   // advances every live path by one segment.
-  const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / kWfIters + 4;
+  const uint64_t max_batches = (uint64_t)ta.total_units * ta.chunk * (ta.max_depth + 1ull) / (uint64_t)(iters * passes) + 4;
   // Wall-clock guard as well (300 s; development knob RTW_WF_TIMEOUT_S): a
   // queue that never drains is reported instead of hanging the caller.
   const char* tos = dev_knob("RTW_WF_TIMEOUT_S");
@@ -913,8 +918,8 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       if (S.done) continue;
       rtwk::WfArgs<R>& a = S.a;
       hipError_t e = hipSuccess;
-      for (int i = 0; i < kWfIters && e == hipSuccess; ++i) {
-        const bool even = (i & 1) == 0;
+      for (int i = 0; i < iters && e == hipSuccess; ++i) {
+        const bool even = (i & 1) == 0 || (passes & 1u) == 0u;  // (an even pass count returns to its input queue)
         a.in = even ? S.qa : S.qb;
         a.out = even ? S.qb : S.qa;
         a.seg_in = even ? S.seg_a : S.seg_b;

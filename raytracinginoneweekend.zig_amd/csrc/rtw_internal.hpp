@@ -190,6 +190,7 @@ struct WfArgs {
   uint32_t n_slots, n_segs;
   uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
   uint32_t bounces;    // wf_step: bounce segments per path per launch (>= 1), the path kept in registers between them
+  uint32_t passes;     // wf_step: queue passes per launch (>= 1): in -> out, out -> in, ... (every segment through the queues)
 };
 
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);

@@ -169,6 +169,19 @@ __device__ __forceinline__ uint32_t chunk_end(const TraceArgs<R>& A, uint32_t c)
   return min(c * A.chunk + A.chunk, A.spp);
 }
 
+// A wave-uniform word this wave may have written earlier in the same launch:
+// a vector load at device scope (past the CU's L1), not a scalar load (the
+// scalar cache does not see vector stores).
+__device__ __forceinline__ uint32_t ld_wave_u32(const uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Between two queue passes of one launch: this wave's stores have completed
+// before it reads the lines back (workgroup scope: the same CU's L1, which its
+// own stores keep current; no L2 write-back).
+__device__ __forceinline__ void wave_own_writes_visible() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
 // Waves are persistent over segments: wave w owns segments w, w + nwaves, ...
 // for the whole frame (the host launches the same grid every time).
 __device__ __forceinline__ uint32_t wave_id() { return blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6); }
@@ -462,21 +475,25 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
   const WfArgs<R>& A = wkargs<R>();  // (A_arg is the same record, read where used)
   const uint32_t lid = lane_id();
   if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
-    if (lid == 0)
+    if (lid == 0 && (A.passes & 1u) != 0u)  // (an even pass count ends in seg_in, already all zero)
       for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) A.seg_out[seg] = 0u;
     return;
   }
   const LdsTables<R> T = stage_tables<R>(A.t.sc, lds_raw);
   KStats st;
   static_assert(kSegCap == 64, "one path per lane per segment");
-  auto step_segment = [&](uint32_t seg) {
-    const uint32_t n_in = A.seg_in[seg];
+  // One queue pass over a segment: qin -> qout.  The segment's count and
+  // reservoir are read with vector loads (a later pass of this launch reads
+  // what lane 0 wrote in the pass before; the scalar cache would not see it).
+  auto step_segment = [&](uint32_t seg, const PathBuf<R>& qin, const PathBuf<R>& qout, const uint32_t* sin,
+                          uint32_t* sout) {
+    const uint32_t n_in = ld_wave_u32(sin + seg);
     if (n_in == 0u) {
-      if (lid == 0) A.seg_out[seg] = 0u;
+      if (lid == 0) sout[seg] = 0u;
       return;
     }
     const uint32_t base = seg * kSegCap;
-    uint32_t qnext = A.seg_resv[2 * seg], qend = A.seg_resv[2 * seg + 1], out_n = 0;
+    uint32_t qnext = ld_wave_u32(A.seg_resv + 2 * seg), qend = ld_wave_u32(A.seg_resv + 2 * seg + 1), out_n = 0;
     const uint32_t i = base + lid;
     const bool valid = lid < n_in;
     Lane<R> L{};
@@ -485,9 +502,9 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
     int hit = -1;
     R tmax = (R)0;
     if (valid) {
-      load_path(A.in, i, L, slot);
-      hit = A.in.hk[i];
-      tmax = A.in.ht[i];
+      load_path(qin, i, L, slot);
+      hit = qin.hk[i];
+      tmax = qin.ht[i];
     }
     // A.bounces (>= 1) bounce segments per path in this launch: shade, then
     // the next ray's closest hit, with the path kept in registers between
@@ -503,9 +520,9 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
       if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
       if (!wany(live)) break;
     }
-    push_path_hit(A.out, base, out_n, live, L, slot, nh, nt);
+    push_path_hit(qout, base, out_n, live, L, slot, nh, nt);
     if (lid == 0) {
-      A.seg_out[seg] = out_n;
+      sout[seg] = out_n;
       A.seg_resv[2 * seg] = qnext;
       A.seg_resv[2 * seg + 1] = qend;
     }
@@ -513,7 +530,19 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
   // (Segments dealt at run time instead, one ticket of a device counter per
   // segment, was 2.5x slower: ~16K same-address atomics per launch serialise
   // at ~8.5 ns each; profiles/r03/wf_dynamic_ab.txt.)
-  for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) step_segment(seg);
+  // A.passes queue passes per launch: in -> out, out -> in, ...  A wave owns
+  // its segments for the whole frame and a path never leaves its segment, so
+  // a pass needs only this wave's own writes of the pass before: every path
+  // still crosses the queues once per A.bounces segments, without the launch.
+  for (uint32_t q = 0; q < A.passes; ++q) {
+    const bool odd = (q & 1u) != 0u;
+    const PathBuf<R>& qin = odd ? A.out : A.in;
+    const PathBuf<R>& qout = odd ? A.in : A.out;
+    const uint32_t* sin = odd ? A.seg_out : A.seg_in;
+    uint32_t* sout = odd ? A.seg_in : A.seg_out;
+    if (q > 0) wave_own_writes_visible();
+    for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) step_segment(seg, qin, qout, sin, sout);
+  }
 }
 
 // ------------------------------------------------------------------ finish --

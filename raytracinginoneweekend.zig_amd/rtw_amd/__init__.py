@@ -30,6 +30,7 @@ PRECISION = {"f64": 0, "f32": 1}
 ENGINE = {"megakernel": 0, "wavefront": 1}
 DEFAULT_WF_PATHS = 3 << 18  # rtw_hip.h RTW_DEFAULT_WF_PATHS
 DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (params.wf_sets overrides)
+DEFAULT_WF_PASSES = 8  # rtw_hip.h RTW_DEFAULT_WF_PASSES (params.wf_passes overrides)
 WF_DRAIN = {"samples": 0, "slots": 1, "none": 2}  # rtw_wf_drain
 WF_FORM = {"fused": 0, "split": 1}  # rtw_wf_form
 WORLD_FEATURES = {"auto": 0, "all": 1}  # rtw_world_features
@@ -72,7 +73,7 @@ class Params(C.Structure):
                 ("engine", C.c_uint32), ("wf_paths", C.c_uint32),
                 ("wf_sets", C.c_uint32), ("wf_drain", C.c_uint32), ("wf_form", C.c_uint32),
                 ("world_waves", C.c_uint32), ("world_features", C.c_uint32), ("world_traversal", C.c_uint32),
-                ("wf_bounces", C.c_uint32), ("reserved", C.c_uint32)]
+                ("wf_bounces", C.c_uint32), ("wf_passes", C.c_uint32)]
 
 
 _lib = None
@@ -179,7 +180,7 @@ def cover_scene(seed: int = 42):
 def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACKGROUND, row_begin=0,
                 row_stride=1, row_count=None, chunk=0, precision="f64", device=-1, engine="megakernel",
                 wf_paths=0, wf_sets=0, wf_drain="samples", wf_form="fused", world_waves=0,
-                world_features="auto", world_traversal="auto", wf_bounces=0) -> Params:
+                world_features="auto", world_traversal="auto", wf_bounces=0, wf_passes=0) -> Params:
     """rtw_params (ABI v4): every engine choice is a field (0 / the first
     name = the library default); nothing is read from the environment."""
     if row_count is None:
@@ -192,7 +193,7 @@ def make_params(width, height, spp, max_depth=50, seed=42, background=COVER_BACK
     return Params(width, height, spp, max_depth, seed, (C.c_double * 3)(*background), row_begin, row_stride,
                   row_count, chunk, prec, device, eng, wf_paths, wf_sets, enum(wf_drain, WF_DRAIN),
                   enum(wf_form, WF_FORM), world_waves, enum(world_features, WORLD_FEATURES),
-                  enum(world_traversal, WORLD_TRAVERSAL), wf_bounces, 0)
+                  enum(world_traversal, WORLD_TRAVERSAL), wf_bounces, wf_passes)
 
 
 def _arr(x, typ):

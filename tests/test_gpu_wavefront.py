@@ -29,11 +29,13 @@ def drain(request):
     return request.param
 
 
-@pytest.fixture(params=["fused", "split"])
+@pytest.fixture(params=["fused", "fused1", "split"])
 def engine_form(request):
     """... and both forms of the engine (params.wf_form): one fused kernel per
     bounce (shade + the next closest hit, the default) and separate extend /
-    shade kernels."""
+    shade kernels; the fused form with the default queue passes per launch
+    (params.wf_passes: a wave moves its segments through the queues pass after
+    pass inside one launch) and with one pass per launch ("fused1")."""
     return request.param
 
 
@@ -50,8 +52,9 @@ def wf_config(rtw, monkeypatch, drain, engine_form, queue_sets):
     """The engine configuration travels in rtw_params (ABI v4): every params
     the test makes carries this case's wf_drain / wf_form / wf_sets."""
     orig = rtw.make_params
-    cfg = dict(wf_drain={"samples": "samples", "finish": "slots", "queues": "none"}[drain], wf_form=engine_form,
-               wf_sets=queue_sets)
+    cfg = dict(wf_drain={"samples": "samples", "finish": "slots", "queues": "none"}[drain],
+               wf_form="split" if engine_form == "split" else "fused", wf_sets=queue_sets,
+               wf_passes=1 if engine_form == "fused1" else 0)
 
     def make_params(*a, **kw):
         for k, v in cfg.items():
@@ -69,9 +72,9 @@ def cover(rtw, oracle):
 
 def both(rtw, cam, sph, mats, **kw):
     """(megakernel rgb, mean), (wavefront rgb, mean) for the same params."""
-    wf_paths = kw.pop("wf_paths", 0)
+    wf = {k: kw.pop(k) for k in ("wf_paths", "wf_passes") if k in kw}
     a = rtw.render(cam, sph, mats, rtw.make_params(**kw), want_mean=True)
-    b = rtw.render(cam, sph, mats, rtw.make_params(engine="wavefront", wf_paths=wf_paths, **kw), want_mean=True)
+    b = rtw.render(cam, sph, mats, rtw.make_params(engine="wavefront", **wf, **kw), want_mean=True)
     return a, b
 
 
@@ -92,6 +95,18 @@ def test_wavefront_cover_parity(rtw, oracle, cover, precision, w, spp, chunk, pa
     assert_identical(mk, wf, f"wavefront vs megakernel {precision} {w}x{h}x{spp} paths {paths}")
     o = oracle_render(oracle, osc, ocam, **kw)
     assert_parity(wf[0], o, f"wavefront {precision} {w}x{h}x{spp} chunk {chunk} paths {paths}")
+
+
+@pytest.mark.parametrize("passes", [2, 3, 64])
+def test_wavefront_queue_passes_per_launch(rtw, cover, passes):
+    """params.wf_passes other than the default (8) and 1: an even count
+    returns each launch's output to its input queue, an odd count alternates
+    the queues per launch as one pass does; 64 (the maximum) lets a batch run
+    past the drain trigger.  Same image as the megakernel."""
+    sph, mats, cam, _, _ = cover
+    kw = dict(width=400, height=rtw.image_height(400, ASPECT), spp=16)
+    mk, wf = both(rtw, cam, sph, mats, wf_paths=4096, wf_passes=passes, **kw)
+    assert_identical(mk, wf, f"wf_passes {passes}")
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2, 5])

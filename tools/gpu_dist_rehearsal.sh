@@ -7,5 +7,5 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 RTW_DIST_BACKEND=gloo RTW_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
-  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 \
+  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 \
   > gpurun_out/dist_rehearsal.json 2> gpurun_out/dist_rehearsal.err

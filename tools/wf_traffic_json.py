@@ -15,6 +15,7 @@ frames = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4].isdigit() else 1
 KERNELS = ("wf_extend", "wf_shade", "wf_step", "wf_finish", "wf_drain")
 FUSED = "--split" not in sys.argv  # the engine form the passes ran (params.wf_form)
 SETS = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--sets=")), 2)  # params.wf_sets
+PASSES = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--passes=")), 8)  # params.wf_passes (fused)
 
 
 def total(d, name):
@@ -34,7 +35,8 @@ wk, wper = total(write_dir, "WRITE_SIZE")
 if fk == 0 or wk == 0:
     sys.exit("no bounce-kernel counter rows")
 res = {"config": {"width": 1200, "height": 675, "spp": 500, "precision": "f64", "engine": "wavefront",
-                  "fused": FUSED, "sets": SETS, "wf_paths": 0},
+                  "fused": FUSED, "sets": SETS, "wf_paths": 0,
+                  "passes": PASSES if FUSED else 1, "bounces": 1},
        "fetch_size_kb_per_frame": fk / frames, "write_size_kb_per_frame": wk / frames,
        "per_kernel_bytes_per_frame": {k: (2 * fper.get(k, 0.0) + wper.get(k, 0.0)) * 1024 / frames for k in KERNELS},
        "traffic_bytes_per_frame": (2 * fk + wk) * 1024 / frames,
