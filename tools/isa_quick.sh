@@ -1,5 +1,5 @@
 #!/bin/bash
 # Device ISA of the product variants only (var 0 / 8, mode 0) -> build/quick.s, then VGPR report.
 cd "$(dirname "$0")/../raytracinginoneweekend.zig_amd" && mkdir -p build &&
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I../include -Icsrc -DRTW_ISA_QUICK \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -mllvm -amdgpu-sched-strategy=iterative-ilp -I../include -Icsrc -DRTW_ISA_QUICK \
   --cuda-device-only -S csrc/rtw_trace.hip -o build/quick.s "$@" 2>&1 | grep -E "error" ; python ../tools/vgprs.py build/quick.s
