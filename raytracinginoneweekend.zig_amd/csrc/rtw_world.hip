@@ -590,8 +590,7 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
       continue;
     }
     if (MODE == 1 && lid == 0) ++wl;
-    static_assert(kMaxLeafPrims <= 2, "trav_phase tests leaves of <= 2 primitives");
-    if (lf != kNoRef) {  // 1 or 2 primitives (kMaxLeafPrims)
+    if (lf != kNoRef) {  // 1 .. kMaxLeafPrims primitives
       static_assert(kWorldRec * sizeof(D) == 128, "primitive record size");
       const uint32_t first = lf & 0x7FFFFFu, cnt = (lf >> 23) & kLeafCountMask;
       for (uint32_t k = first; k < first + cnt; ++k) {

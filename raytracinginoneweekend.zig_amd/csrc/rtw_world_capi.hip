@@ -99,9 +99,19 @@ struct Bvh {
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
 };
 
+// Leaf size: worlds of >= kLeafOneMin primitives (those AUTO walks per lane:
+// >= 2 x kLaneNodes) get leaves of ONE primitive, smaller ones kMaxLeafPrims.
+// Per lane, a leaf's primitives are tested one after another by the lanes
+// that reach it: the globe at leaf 1 vs 2 is +4.3 % (1.98 vs 3.45 primitive
+// tests, 17.6 vs 16.3 node visits per segment), 10 of 10 alternations; leaves
+// of 3 and 4 are slower; the union walk on scene 1 (48 primitives) prefers 2
+// (-6 % at 1): profiles/r05/world_leaf_ab.txt.
+constexpr size_t kLeafOneMin = 512;
+
 class Builder {
  public:
-  Builder(const std::vector<Box>& boxes, Bvh& out) : boxes_(boxes), out_(out) {
+  Builder(const std::vector<Box>& boxes, Bvh& out)
+      : boxes_(boxes), out_(out), leaf_max_(boxes.size() >= kLeafOneMin ? 1u : rtwk::kMaxLeafPrims) {
     idx_.resize(boxes.size());
     for (size_t i = 0; i < idx_.size(); ++i) idx_[i] = (uint32_t)i;
     for (const Box& b : boxes) {
@@ -119,6 +129,7 @@ class Builder {
  private:
   const std::vector<Box>& boxes_;
   Bvh& out_;
+  const uint32_t leaf_max_;  // primitives per leaf (<= rtwk::kMaxLeafPrims)
   std::vector<uint32_t> idx_;
   std::vector<std::array<double, 3>> cent_;
 
@@ -193,7 +204,7 @@ class Builder {
   uint32_t child(uint32_t b, uint32_t e, uint32_t depth) {
     // Leaves: few primitives, or the depth cap of the per-lane LDS stack
     // (node() switches to median splits while they still fit the cap).
-    if (e - b <= rtwk::kMaxLeafPrims || (depth >= rtwk::kBvhStack - 1 && e - b <= rtwk::kLeafCountMask))
+    if (e - b <= leaf_max_ || (depth >= rtwk::kBvhStack - 1 && e - b <= rtwk::kLeafCountMask))
       return leaf(b, e);
     const uint32_t n = alloc();
     node(n, b, e, depth);
@@ -202,12 +213,12 @@ class Builder {
   void node(uint32_t n, uint32_t b, uint32_t e, uint32_t depth) {
     out_.max_depth = std::max(out_.max_depth, depth + 1);
     uint32_t m;
-    if (e - b <= rtwk::kMaxLeafPrims) {  // root of a tiny world: one leaf + an empty one
+    if (e - b <= leaf_max_) {  // root of a tiny world: one leaf + an empty one
       m = e;
     } else {
       // SAH while the median-split depth of the rest still fits the stack.
       uint32_t need = 0;
-      for (uint32_t c = e - b; c > rtwk::kMaxLeafPrims; c = (c + 1) / 2) ++need;
+      for (uint32_t c = e - b; c > leaf_max_; c = (c + 1) / 2) ++need;
       m = split(b, e, depth + need + 2 < rtwk::kBvhStack);
     }
     // Child 0 is built first, so an interior child 0 is record n + 1, the line
@@ -586,7 +597,7 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   // AUTO: per lane on BVHs of >= kLaneNodes nodes (configs[4]'s globe: 5,802
   // nodes, +30 %); the union walk on small trees, where the lanes' paths
   // mostly coincide (scene 1's 23 nodes: the union 17 % faster).
-  const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= 2u;
+  const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= rtwk::kMaxLeafPrims;
   const bool lane = lane_ok && (p->world_traversal == RTW_WORLD_TRAVERSAL_LANE ||
                                 (p->world_traversal == RTW_WORLD_TRAVERSAL_AUTO && w->view.n_nodes >= kLaneNodes));
   c.fs = rtwk::world_feature_set(feat, lane);
