@@ -61,6 +61,8 @@ constexpr int kFeatAll = kFeatNoise | kFeatImage | kFeatXform | kFeatRect;
 // Not a world feature: the sphere-world instantiation that traverses the BVH
 // per lane (closest_lane) instead of as the wave's union (closest).
 constexpr int kFeatLane = 16;
+// ... on the 4-wide BVH (WorldView.node4), with 16-bit stack entries.
+constexpr int kFeatWide = 32;
 
 __device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
 
@@ -511,20 +513,40 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
   // once per phase (re-read in the loop, the scalar load's lgkmcnt wait also
   // waited for the stack pop's LDS read, which `top` is there to hide)
   using GF = const __attribute__((address_space(1))) float;  // global: vector memory loads, not flat
-  GF* nodes = (GF*)W.node;
+  constexpr bool WIDE = (FEAT & kFeatWide) != 0;  // the 4-wide BVH (WorldView.node4), 16-bit stack entries
+  GF* nodes = (GF*)(WIDE ? W.node4 : W.node);
   using GD = const __attribute__((address_space(1))) D;
   GD* pr = (GD*)W.prim;
   asm volatile("" : "+s"(nodes), "+s"(pr));
   const RaySp ws = ray_space(o, d, W.flags);
   // the stack's top entry lives in a register (`top`, kNoRef when empty;
   // entries below it in LDS): a pop waits on no LDS read
+  // WIDE: 16-bit entries, entry e of lane l in half (e & 1) of word (e >> 1) * 64 + l (a lane
+  // touches only its own words); interior refs as they are (< 2^15 nodes), a leaf of one
+  // primitive as 0x8000 | its first primitive (< 2^15): rtw_world_capi.hip collapse4.
+  uint16_t* const s16 = reinterpret_cast<uint16_t*>(lstack);
+  auto slot16 = [&](uint32_t e) { return s16 + ((((e >> 1) * 64u + lid) << 1) | (e & 1u)); };
   auto pop = [&]() -> uint32_t {
     const uint32_t r = top;
-    top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
+    if constexpr (WIDE) {
+      if (sp) {
+        const uint32_t v = *slot16(--sp);
+        top = (v & 0x8000u) ? (kLeafBit | (1u << 23) | (v & 0x7FFFu)) : v;
+      } else {
+        top = kNoRef;
+      }
+    } else {
+      top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
+    }
     return r;
   };
   auto push = [&](uint32_t r) {
-    if (top != kNoRef) lstack[(sp++) * 64u + lid] = top;
+    if (top != kNoRef) {
+      if constexpr (WIDE)
+        *slot16(sp++) = (uint16_t)(top < kLeafBit ? top : (0x8000u | (top & 0x7FFFu)));
+      else
+        lstack[(sp++) * 64u + lid] = top;
+    }
     top = r;
   };
   bool yielded = false;
@@ -543,7 +565,51 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
         break;
       }
       if (MODE == 1 && lid == 0) ++wi;
-      if (step) {
+      if (WIDE && step) {
+        if (MODE == 1) ++nv;
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
+            reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 7));
+        // lo x / y / z and hi x / y / z of the 4 children, then their refs
+        const f4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+        float key[4];
+        uint32_t r[4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // children {2q, 2q + 1}: one packed slab step per bound
+          const f2 x0 = pfma(f2{lx[2 * q], lx[2 * q + 1]}, ix, oxl), x1 = pfma(f2{hx[2 * q], hx[2 * q + 1]}, ix, oxh);
+          const f2 y0 = pfma(f2{ly[2 * q], ly[2 * q + 1]}, iy, oyl), y1 = pfma(f2{hy[2 * q], hy[2 * q + 1]}, iy, oyh);
+          const f2 z0 = pfma(f2{lz[2 * q], lz[2 * q + 1]}, iz, ozl), z1 = pfma(f2{hz[2 * q], hz[2 * q + 1]}, iz, ozh);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int k = 2 * q + c;
+            const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), max_q(fminf(z0[c], z1[c]), tminf));
+            const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), min_q(fmaxf(z0[c], z1[c]), tmaxf));
+            r[k] = __float_as_uint(rf[k]);
+            // a hit child's key is its entry distance (finite: the sort's +inf means "missed"); an
+            // absent child (kNoRef, empty box) never hits
+            key[k] = (n <= f && r[k] != kNoRef) ? fminf(n, 3.4028235e38f) : __builtin_inff();
+          }
+        }
+        // nearest first: sort the 4 (key, ref) pairs ascending (5 compare-exchanges), push
+        // the farther hit children farthest first, descend into the nearest
+        auto ce = [&](int a, int b) {
+          const bool sw = key[b] < key[a];
+          const float ka = key[a];
+          const uint32_t ra = r[a];
+          key[a] = sw ? key[b] : ka, r[a] = sw ? r[b] : ra;
+          key[b] = sw ? ka : key[b], r[b] = sw ? ra : r[b];
+        };
+        ce(0, 1), ce(2, 3), ce(0, 2), ce(1, 3), ce(1, 2);
+        if (key[3] < __builtin_inff()) push(r[3]);
+        if (key[2] < __builtin_inff()) push(r[2]);
+        if (key[1] < __builtin_inff()) push(r[1]);
+        const uint32_t nx = key[0] < __builtin_inff() ? r[0] : kNoRef;
+        ref = nx != kNoRef ? nx : pop();
+        if (ref != kNoRef && ref >= kLeafBit && pend == kNoRef) {  // postpone the leaf, keep walking
+          pend = ref;
+          ref = pop();
+        }
+      } else if (step) {
         if (MODE == 1) ++nv;
         // (a 32-bit byte offset from the SGPR base: the loads' saddr form, no 64-bit address math)
         typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1134,13 +1200,16 @@ static void launch_feat(const WorldArgs& a, uint32_t grid, size_t lds, hipStream
 // Instantiated feature sets: spheres with solid / checker / image textures
 // (scenes 1, 2, 4 and configs[4]'s globe), rects + transforms + lights without
 // noise / image (the Cornell box, scene 5's light), and everything.
-int world_feature_set(uint32_t feat, bool lane) {
-  if ((feat & ~(uint32_t)kFeatImage) == 0u) return lane ? (kFeatImage | kFeatLane) : kFeatImage;
+int world_feature_set(uint32_t feat, bool lane, bool wide) {
+  if ((feat & ~(uint32_t)kFeatImage) == 0u)
+    return lane ? (wide ? (kFeatImage | kFeatLane | kFeatWide) : (kFeatImage | kFeatLane)) : kFeatImage;
   if ((feat & ~(uint32_t)(kFeatXform | kFeatRect)) == 0u) return kFeatXform | kFeatRect;
   return kFeatAll;
 }
 hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs) {
-  if (fs == (kFeatImage | kFeatLane))
+  if (fs == (kFeatImage | kFeatLane | kFeatWide))
+    launch_feat<kFeatImage | kFeatLane | kFeatWide>(a, grid, lds, s, mode, occ);
+  else if (fs == (kFeatImage | kFeatLane))
     launch_feat<kFeatImage | kFeatLane>(a, grid, lds, s, mode, occ);
   else if (fs == kFeatImage)
     launch_feat<kFeatImage>(a, grid, lds, s, mode, occ);
@@ -1164,6 +1233,7 @@ static int bpc_feat(size_t lds, int occ) {
   return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 int world_blocks_per_cu(size_t lds, int occ, int fs) {
+  if (fs == (kFeatImage | kFeatLane | kFeatWide)) return bpc_feat<kFeatImage | kFeatLane | kFeatWide>(lds, occ);
   if (fs == (kFeatImage | kFeatLane)) return bpc_feat<kFeatImage | kFeatLane>(lds, occ);
   if (fs == kFeatImage) return bpc_feat<kFeatImage>(lds, occ);
   if (fs == (kFeatXform | kFeatRect)) return bpc_feat<kFeatXform | kFeatRect>(lds, occ);
