@@ -516,7 +516,7 @@ int validate(const rtw_params* p) {
   if (p->wf_form > RTW_WF_SPLIT) return fail(RTW_EINVAL, "wf_form %u", p->wf_form);
   if (p->world_waves > 4) return fail(RTW_EINVAL, "world_waves %u outside [0, 4]", p->world_waves);
   if (p->world_features > RTW_WORLD_FEATURES_ALL) return fail(RTW_EINVAL, "world_features %u", p->world_features);
-  if (p->world_traversal > RTW_WORLD_TRAVERSAL_LANE_BVH2) return fail(RTW_EINVAL, "world_traversal %u", p->world_traversal);
+  if (p->world_traversal > RTW_WORLD_TRAVERSAL_LANE) return fail(RTW_EINVAL, "world_traversal %u", p->world_traversal);
   if (p->wf_bounces > 16) return fail(RTW_EINVAL, "wf_bounces %u outside [0, 16]", p->wf_bounces);
   if (p->wf_passes > 64) return fail(RTW_EINVAL, "wf_passes %u outside [0, 64]", p->wf_passes);
   if (p->engine == RTW_ENGINE_WAVEFRONT && (p->wf_paths > (1u << 28) || (p->wf_paths && p->wf_paths < 64)))

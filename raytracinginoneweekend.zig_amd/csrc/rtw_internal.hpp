@@ -251,7 +251,6 @@ constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder c
 // a BVH of depth <= kLaneStack never overflows it (a push per level at most);
 // deeper BVHs take the union walk
 constexpr uint32_t kLaneStack = 16;
-constexpr uint32_t kNode4Words = 32;  // 4-wide BVH node record: 6 x 4 bounds, 4 refs, padding (128 B)
 #ifndef RTW_MAX_LEAF_PRIMS
 #define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
 #endif
@@ -268,7 +267,6 @@ struct WorldView {
   const float* node;
   const uint32_t* order;
   const float* cull;             // leaf pretest records (kCullBit leaves)
-  const float* node4;            // the 4-wide BVH for the per-lane walk (kNode4Words per node), or null
   uint32_t n_prims, n_nodes, n_perlins, flags;
   float cull_cmax, cull_rho;     // rtw_cull.hpp Cmax and rho_max over the pretested spheres
 };
@@ -289,7 +287,7 @@ constexpr uint32_t kTailWin = 32;  // world kernel: the last samples of a unit o
 // fs: the kernel's feature set, world_feature_set(features of the world, per-lane
 // traversal): bits 1 noise texture, 2 image texture, 4 transform chains, 8 rects,
 // 16 per-lane BVH traversal (sphere worlds only).
-int world_feature_set(uint32_t feat, bool lane, bool wide);
+int world_feature_set(uint32_t feat, bool lane, bool packed);
 hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs);
 int world_blocks_per_cu(size_t lds, int occ, int fs);
 constexpr int kWorldBlock = 256;

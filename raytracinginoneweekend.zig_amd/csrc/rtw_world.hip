@@ -61,8 +61,8 @@ constexpr int kFeatAll = kFeatNoise | kFeatImage | kFeatXform | kFeatRect;
 // Not a world feature: the sphere-world instantiation that traverses the BVH
 // per lane (closest_lane) instead of as the wave's union (closest).
 constexpr int kFeatLane = 16;
-// ... on the 4-wide BVH (WorldView.node4), with 16-bit stack entries.
-constexpr int kFeatWide = 32;
+// ... reading each child's ref from its lower bounds' low bits (rtw_world_capi.hip pack_refs).
+constexpr int kFeatPacked = 32;
 
 __device__ __forceinline__ const uint32_t* meta_of(const D* r) { return reinterpret_cast<const uint32_t*>(r + 14); }
 
@@ -513,40 +513,24 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
   // once per phase (re-read in the loop, the scalar load's lgkmcnt wait also
   // waited for the stack pop's LDS read, which `top` is there to hide)
   using GF = const __attribute__((address_space(1))) float;  // global: vector memory loads, not flat
-  constexpr bool WIDE = (FEAT & kFeatWide) != 0;  // the 4-wide BVH (WorldView.node4), 16-bit stack entries
-  GF* nodes = (GF*)(WIDE ? W.node4 : W.node);
+  GF* nodes = (GF*)W.node;
+  // PACKED: refs in the lower bounds' low bits, as 18 bits (rtw_world_capi.hip pack_refs): a leaf
+  // is LB | (count - 1) << 16 | first; the walk keeps refs in that form (kNoRef stays kNoRef).
+  constexpr bool PACKED = (FEAT & kFeatPacked) != 0;
+  constexpr uint32_t LB = PACKED ? 0x20000u : kLeafBit;
   using GD = const __attribute__((address_space(1))) D;
   GD* pr = (GD*)W.prim;
   asm volatile("" : "+s"(nodes), "+s"(pr));
   const RaySp ws = ray_space(o, d, W.flags);
   // the stack's top entry lives in a register (`top`, kNoRef when empty;
   // entries below it in LDS): a pop waits on no LDS read
-  // WIDE: 16-bit entries, entry e of lane l in half (e & 1) of word (e >> 1) * 64 + l (a lane
-  // touches only its own words); interior refs as they are (< 2^15 nodes), a leaf of one
-  // primitive as 0x8000 | its first primitive (< 2^15): rtw_world_capi.hip collapse4.
-  uint16_t* const s16 = reinterpret_cast<uint16_t*>(lstack);
-  auto slot16 = [&](uint32_t e) { return s16 + ((((e >> 1) * 64u + lid) << 1) | (e & 1u)); };
   auto pop = [&]() -> uint32_t {
     const uint32_t r = top;
-    if constexpr (WIDE) {
-      if (sp) {
-        const uint32_t v = *slot16(--sp);
-        top = (v & 0x8000u) ? (kLeafBit | (1u << 23) | (v & 0x7FFFu)) : v;
-      } else {
-        top = kNoRef;
-      }
-    } else {
-      top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
-    }
+    top = sp ? lstack[(--sp) * 64u + lid] : kNoRef;
     return r;
   };
   auto push = [&](uint32_t r) {
-    if (top != kNoRef) {
-      if constexpr (WIDE)
-        *slot16(sp++) = (uint16_t)(top < kLeafBit ? top : (0x8000u | (top & 0x7FFFu)));
-      else
-        lstack[(sp++) * 64u + lid] = top;
-    }
+    if (top != kNoRef) lstack[(sp++) * 64u + lid] = top;
     top = r;
   };
   bool yielded = false;
@@ -557,7 +541,7 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     // keeps walking; the phase ends once every lane holds a leaf or is out of
     // work (speculative while-while): the leaf tests then run with most lanes busy.
     for (;;) {
-      const bool step = ref < kLeafBit;
+      const bool step = ref < LB;
       if (!wany(step & (pend == kNoRef))) break;
       const uint32_t nact = popc64(wballot((ref != kNoRef) | (pend != kNoRef)));
       if (nact < yield_lanes && nact < start) {
@@ -565,57 +549,13 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
         break;
       }
       if (MODE == 1 && lid == 0) ++wi;
-      if (WIDE && step) {
-        if (MODE == 1) ++nv;
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
-            reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 7));
-        // lo x / y / z and hi x / y / z of the 4 children, then their refs
-        const f4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
-        float key[4];
-        uint32_t r[4];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {  // children {2q, 2q + 1}: one packed slab step per bound
-          const f2 x0 = pfma(f2{lx[2 * q], lx[2 * q + 1]}, ix, oxl), x1 = pfma(f2{hx[2 * q], hx[2 * q + 1]}, ix, oxh);
-          const f2 y0 = pfma(f2{ly[2 * q], ly[2 * q + 1]}, iy, oyl), y1 = pfma(f2{hy[2 * q], hy[2 * q + 1]}, iy, oyh);
-          const f2 z0 = pfma(f2{lz[2 * q], lz[2 * q + 1]}, iz, ozl), z1 = pfma(f2{hz[2 * q], hz[2 * q + 1]}, iz, ozh);
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int k = 2 * q + c;
-            const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), max_q(fminf(z0[c], z1[c]), tminf));
-            const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), min_q(fmaxf(z0[c], z1[c]), tmaxf));
-            r[k] = __float_as_uint(rf[k]);
-            // a hit child's key is its entry distance (finite: the sort's +inf means "missed"); an
-            // absent child (kNoRef, empty box) never hits
-            key[k] = (n <= f && r[k] != kNoRef) ? fminf(n, 3.4028235e38f) : __builtin_inff();
-          }
-        }
-        // nearest first: sort the 4 (key, ref) pairs ascending (5 compare-exchanges), push
-        // the farther hit children farthest first, descend into the nearest
-        auto ce = [&](int a, int b) {
-          const bool sw = key[b] < key[a];
-          const float ka = key[a];
-          const uint32_t ra = r[a];
-          key[a] = sw ? key[b] : ka, r[a] = sw ? r[b] : ra;
-          key[b] = sw ? ka : key[b], r[b] = sw ? ra : r[b];
-        };
-        ce(0, 1), ce(2, 3), ce(0, 2), ce(1, 3), ce(1, 2);
-        if (key[3] < __builtin_inff()) push(r[3]);
-        if (key[2] < __builtin_inff()) push(r[2]);
-        if (key[1] < __builtin_inff()) push(r[1]);
-        const uint32_t nx = key[0] < __builtin_inff() ? r[0] : kNoRef;
-        ref = nx != kNoRef ? nx : pop();
-        if (ref != kNoRef && ref >= kLeafBit && pend == kNoRef) {  // postpone the leaf, keep walking
-          pend = ref;
-          ref = pop();
-        }
-      } else if (step) {
+      if (step) {
         if (MODE == 1) ++nv;
         // (a 32-bit byte offset from the SGPR base: the loads' saddr form, no 64-bit address math)
         typedef float f4 __attribute__((ext_vector_type(4)));
         const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
             reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 6));
-        const f4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        const f4 q0 = nd[0], q1 = nd[1], q2 = nd[2];
         // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3, refs in words 12-13
         const f2 x0 = pfma(f2{q0.x, q0.y}, ix, oxl), x1 = pfma(f2{q1.z, q1.w}, ix, oxh);
         const f2 y0 = pfma(f2{q0.z, q0.w}, iy, oyl), y1 = pfma(f2{q2.x, q2.y}, iy, oyh);
@@ -629,7 +569,16 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
           tn[c] = n;
           hit[c] = n <= f;
         }
-        const uint32_t r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
+        uint32_t r0, r1;
+        if constexpr (PACKED) {  // child c's ref: low 6 bits of its lower x / y / z bounds
+          const uint32_t a0 = __float_as_uint(q0.x), a1 = __float_as_uint(q0.y), b0 = __float_as_uint(q0.z),
+                         b1 = __float_as_uint(q0.w), c0 = __float_as_uint(q1.x), c1 = __float_as_uint(q1.y);
+          r0 = (a0 & 63u) | ((b0 & 63u) << 6) | ((c0 & 63u) << 12);
+          r1 = (a1 & 63u) | ((b1 & 63u) << 6) | ((c1 & 63u) << 12);
+        } else {
+          const f4 q3 = nd[3];
+          r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
+        }
         const bool first0 = tn[0] <= tn[1];
         uint32_t nx = hit[0] ? r0 : (hit[1] ? r1 : kNoRef);
         if (hit[0] && hit[1]) {
@@ -637,7 +586,7 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
           nx = first0 ? r0 : r1;
         }
         ref = nx != kNoRef ? nx : pop();
-        if (ref != kNoRef && ref >= kLeafBit && pend == kNoRef) {  // postpone the leaf, keep walking
+        if (ref != kNoRef && ref >= LB && pend == kNoRef) {  // postpone the leaf, keep walking
           pend = ref;
           ref = pop();
         }
@@ -646,7 +595,7 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     if (yielded) break;
     // Leaf tests: the postponed leaf, else a leaf the lane stopped at.
     uint32_t lf = pend;
-    if (lf == kNoRef && ref != kNoRef && ref >= kLeafBit) {
+    if (lf == kNoRef && ref != kNoRef && ref >= LB) {
       lf = ref;
       ref = pop();
     }
@@ -658,7 +607,8 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     if (MODE == 1 && lid == 0) ++wl;
     if (lf != kNoRef) {  // 1 .. kMaxLeafPrims primitives
       static_assert(kWorldRec * sizeof(D) == 128, "primitive record size");
-      const uint32_t first = lf & 0x7FFFFFu, cnt = (lf >> 23) & kLeafCountMask;
+      const uint32_t first = PACKED ? (lf & 0xFFFFu) : (lf & 0x7FFFFFu);
+      const uint32_t cnt = PACKED ? ((lf >> 16) & 1u) + 1u : (lf >> 23) & kLeafCountMask;
       for (uint32_t k = first; k < first + cnt; ++k) {
         if (MODE == 1) ++nt;
         D t;
@@ -1200,15 +1150,15 @@ static void launch_feat(const WorldArgs& a, uint32_t grid, size_t lds, hipStream
 // Instantiated feature sets: spheres with solid / checker / image textures
 // (scenes 1, 2, 4 and configs[4]'s globe), rects + transforms + lights without
 // noise / image (the Cornell box, scene 5's light), and everything.
-int world_feature_set(uint32_t feat, bool lane, bool wide) {
+int world_feature_set(uint32_t feat, bool lane, bool packed) {
   if ((feat & ~(uint32_t)kFeatImage) == 0u)
-    return lane ? (wide ? (kFeatImage | kFeatLane | kFeatWide) : (kFeatImage | kFeatLane)) : kFeatImage;
+    return lane ? (packed ? (kFeatImage | kFeatLane | kFeatPacked) : (kFeatImage | kFeatLane)) : kFeatImage;
   if ((feat & ~(uint32_t)(kFeatXform | kFeatRect)) == 0u) return kFeatXform | kFeatRect;
   return kFeatAll;
 }
 hipError_t launch_world(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ, int fs) {
-  if (fs == (kFeatImage | kFeatLane | kFeatWide))
-    launch_feat<kFeatImage | kFeatLane | kFeatWide>(a, grid, lds, s, mode, occ);
+  if (fs == (kFeatImage | kFeatLane | kFeatPacked))
+    launch_feat<kFeatImage | kFeatLane | kFeatPacked>(a, grid, lds, s, mode, occ);
   else if (fs == (kFeatImage | kFeatLane))
     launch_feat<kFeatImage | kFeatLane>(a, grid, lds, s, mode, occ);
   else if (fs == kFeatImage)
@@ -1233,7 +1183,7 @@ static int bpc_feat(size_t lds, int occ) {
   return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 int world_blocks_per_cu(size_t lds, int occ, int fs) {
-  if (fs == (kFeatImage | kFeatLane | kFeatWide)) return bpc_feat<kFeatImage | kFeatLane | kFeatWide>(lds, occ);
+  if (fs == (kFeatImage | kFeatLane | kFeatPacked)) return bpc_feat<kFeatImage | kFeatLane | kFeatPacked>(lds, occ);
   if (fs == (kFeatImage | kFeatLane)) return bpc_feat<kFeatImage | kFeatLane>(lds, occ);
   if (fs == kFeatImage) return bpc_feat<kFeatImage>(lds, occ);
   if (fs == (kFeatXform | kFeatRect)) return bpc_feat<kFeatXform | kFeatRect>(lds, occ);

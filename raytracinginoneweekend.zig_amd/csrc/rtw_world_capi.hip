@@ -11,7 +11,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -98,73 +97,55 @@ struct Bvh {
   std::vector<float> nodes;  // kNodeWords per node
   std::vector<uint32_t> order;  // stored position -> original prim index
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
-  // The 4-wide form for the per-lane walk (collapse4): kNode4Words per node,
-  // and the deepest its walk's stack can get (sum of (children - 1) on a path).
-  std::vector<float> nodes4;
-  uint32_t n_nodes4 = 0, stack4 = 0;
+  bool packed = false;  // pack_refs: the child refs also in the low bits of the lower bounds
 };
 
-// The binary BVH collapsed two levels per node: a node's children are its
-// binary node's leaf children and its interior children's children (2 to 4).
-// Record (kNode4Words floats = 128 B): lo x[4], lo y[4], lo z[4], hi x[4],
-// hi y[4], hi z[4], refs[4] (kNoRef4 for an absent child), 4 words of padding;
-// the same outward-rounded f32 bounds as the binary records.  Depth-first.
-constexpr uint32_t kNoRef4 = 0xFFFFFFFFu;
-void collapse4(Bvh& b) {
-  b.nodes4.clear();
-  b.n_nodes4 = 0;
-  const float* n2 = b.nodes.data();
-  auto child_box = [&](uint32_t n, int c, float lo[3], float hi[3]) {
-    const float* nd = n2 + (size_t)rtwk::kNodeWords * n;
-    for (int k = 0; k < 3; ++k) lo[k] = nd[2 * k + c], hi[k] = nd[6 + 2 * k + c];
-  };
-  auto child_ref = [&](uint32_t n, int c) {
-    uint32_t r;
-    std::memcpy(&r, n2 + (size_t)rtwk::kNodeWords * n + 12 + c, 4);
-    return r;
-  };
-  // returns {node4 index, stack bound of its walk}
-  std::function<std::pair<uint32_t, uint32_t>(uint32_t)> build = [&](uint32_t n) -> std::pair<uint32_t, uint32_t> {
-    const uint32_t me = b.n_nodes4++;
-    b.nodes4.resize((size_t)b.n_nodes4 * rtwk::kNode4Words, 0.0f);
-    float lo[4][3], hi[4][3];
-    uint32_t ref[4], kids = 0;
-    uint32_t grand[4];  // binary node of an interior child, else kNoRef4
+// The per-lane walk loads a node's 12 bounds (48 B, three 16-B loads) and not
+// its refs (words 12-13): each child's ref, as 18 bits (an interior node
+// index < 2^17, or 0x20000 | (count - 1) << 16 | first primitive < 2^16),
+// rides in the low 6 bits of that child's three lower bounds (words 0 / 2 / 4
+// for child 0, 1 / 3 / 5 for child 1), each moved DOWN to the nearest float
+// whose low bits hold the payload (<= 127 ulps: the box only grows, so the
+// test stays conservative; the union walk reads the same bounds and words
+// 12-13).  The per-lane walk's loads are bound by the vector memory pipeline
+// (TD busy ~0.85, profiles/r05/world_ta_pmc.txt): one load of four per visit.
+uint32_t compact_ref(uint32_t r) {
+  if (r < rtwk::kLeafBit) return r;
+  return 0x20000u | ((((r >> 23) & rtwk::kLeafCountMask) - 1u) << 16) | (r & 0x7FFFFFu);
+}
+float lower_with_low6(float f, uint32_t payload) {  // the largest float <= f whose low 6 bits are `payload`
+  uint32_t b;
+  std::memcpy(&b, &f, 4);
+  if (!(b & 0x80000000u) && b >= 64u && f != 0.0f) {  // positive: smaller bit patterns are smaller
+    uint32_t c = (b & ~63u) | payload;
+    if (c > b) c -= 64u;
+    std::memcpy(&f, &c, 4);
+    return f;
+  }
+  const uint32_t m = b & 0x7FFFFFFFu;  // zero, tiny or negative: a larger magnitude below zero
+  uint32_t c = (m & ~63u) | payload;
+  if (c < m) c += 64u;
+  c |= 0x80000000u;
+  std::memcpy(&f, &c, 4);
+  return f;
+}
+bool pack_refs(Bvh& b, uint32_t n_prims) {
+  if (b.n_nodes >= 0x20000u || n_prims >= 0x10000u || b.max_leaf > 2u) return false;
+  for (uint32_t n = 0; n < b.n_nodes; ++n) {
+    float* nd = b.nodes.data() + (size_t)rtwk::kNodeWords * n;
     for (int c = 0; c < 2; ++c) {
-      const uint32_t r = child_ref(n, c);
-      if (r < rtwk::kLeafBit) {
-        for (int g = 0; g < 2; ++g) {
-          child_box(r, g, lo[kids], hi[kids]);
-          const uint32_t rg = child_ref(r, g);
-          ref[kids] = rg, grand[kids] = rg < rtwk::kLeafBit ? rg : kNoRef4;
-          ++kids;
-        }
-      } else {
-        child_box(n, c, lo[kids], hi[kids]);
-        ref[kids] = r, grand[kids] = kNoRef4;
-        ++kids;
+      uint32_t r;
+      std::memcpy(&r, nd + 12 + c, 4);
+      const uint32_t v = compact_ref(r);
+      for (int k = 0; k < 3; ++k) {
+        const float old = nd[2 * k + c], nw = lower_with_low6(old, (v >> (6 * k)) & 63u);
+        if (!(nw <= old) || !std::isfinite(nw)) return false;  // (never: the bounds are finite)
+        nd[2 * k + c] = nw;
       }
     }
-    uint32_t deepest = 0;
-    for (uint32_t k = 0; k < kids; ++k)
-      if (grand[k] != kNoRef4) {
-        const auto sub = build(grand[k]);
-        ref[k] = sub.first;
-        deepest = std::max(deepest, sub.second);
-      }
-    float* nd = b.nodes4.data() + (size_t)rtwk::kNode4Words * me;
-    for (uint32_t k = 0; k < 4; ++k) {
-      const bool on = k < kids;
-      for (int a = 0; a < 3; ++a) {
-        nd[4 * a + k] = on ? lo[k][a] : INFINITY;        // lo x / y / z
-        nd[12 + 4 * a + k] = on ? hi[k][a] : -INFINITY;  // hi x / y / z
-      }
-      const uint32_t r = on ? ref[k] : kNoRef4;
-      std::memcpy(nd + 24 + k, &r, 4);
-    }
-    return {me, (kids - 1) + deepest};
-  };
-  b.stack4 = build(0).second;
+  }
+  b.packed = true;
+  return true;
 }
 
 // Leaf size: worlds of >= kLeafOneMin primitives (those AUTO walks per lane:
@@ -327,7 +308,7 @@ struct rtw_world_s {
   bool has_moving = false;
   uint32_t feat = 0;  // features used (rtw_world.hip kFeat*): picks the kernel instantiation
   uint32_t info[4] = {0, 0, 0, 0};
-  uint32_t n_nodes4 = 0, stack4 = 0;  // the 4-wide BVH (0 nodes: none)
+  bool packed = false;  // the BVH carries the refs in its bounds' low bits (pack_refs)
 };
 
 extern "C" {
@@ -389,13 +370,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
-    // The 4-wide BVH for the per-lane walk: worlds built with leaves of one
-    // primitive whose refs fit the walk's 16-bit stack entries (rtw_world.hip
-    // trav_phase WIDE) and whose walk fits its 2 x kLaneStack entries.
-    if (bvh.max_leaf == 1 && d->n_prims < 0x8000u) {
-      collapse4(bvh);
-      if (bvh.n_nodes4 >= 0x8000u || bvh.stack4 > 2 * rtwk::kLaneStack) bvh.nodes4.clear(), bvh.n_nodes4 = 0;
-    }
+    (void)pack_refs(bvh, d->n_prims);
     if (flags & RTW_WORLD_DEBUG_BVH) {  // root's two children: leaf (prims) or node, and their boxes
       for (int c = 0; c < 2; ++c) {
         uint32_t ref;
@@ -543,8 +518,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   // (+ two zero padding records: the traversal may load the records after the last)
   const size_t o_order = o_node + al(bvh.nodes.size() * 4 + 2 * (size_t)rtwk::kNodeWords * 4);
   const size_t o_cull = o_order + al((size_t)std::max(n, 1u) * 4);
-  const size_t o_node4 = o_cull + al(std::max(cull.size() * 4, (size_t)4));
-  const size_t total = o_node4 + al(std::max(bvh.nodes4.size() * 4, (size_t)4));
+  const size_t total = o_cull + al(std::max(cull.size() * 4, (size_t)4));
   std::vector<unsigned char> host(total, 0);
   std::memcpy(host.data() + o_prim, prim.data(), prim.size() * 8);
   std::memcpy(host.data() + o_xf, xf.data(), xf.size() * 8);
@@ -558,7 +532,6 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   if (!bvh.nodes.empty()) std::memcpy(host.data() + o_node, bvh.nodes.data(), bvh.nodes.size() * 4);
   if (n) std::memcpy(host.data() + o_order, list_to_pos.data(), (size_t)n * 4);
   if (!cull.empty()) std::memcpy(host.data() + o_cull, cull.data(), cull.size() * 4);
-  if (!bvh.nodes4.empty()) std::memcpy(host.data() + o_node4, bvh.nodes4.data(), bvh.nodes4.size() * 4);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     delete w;
@@ -585,7 +558,6 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.node = reinterpret_cast<const float*>(base + o_node);
   w->view.order = reinterpret_cast<const uint32_t*>(base + o_order);
   w->view.cull = reinterpret_cast<const float*>(base + o_cull);
-  w->view.node4 = bvh.n_nodes4 ? reinterpret_cast<const float*>(base + o_node4) : nullptr;
   w->view.cull_cmax = cull_cmax;
   w->view.cull_rho = cull_rho;
   for (uint32_t i = 0; i < d->n_textures; ++i)
@@ -596,7 +568,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   w->view.n_nodes = bvh.n_nodes;
   w->view.n_perlins = d->n_perlins;
   w->info[0] = bvh.n_nodes, w->info[1] = bvh.n_leaves, w->info[2] = bvh.max_depth, w->info[3] = bvh.max_leaf;
-  w->n_nodes4 = bvh.n_nodes4, w->stack4 = bvh.stack4;
+  w->packed = bvh.packed;
   *out = w;
   return RTW_OK;
 }
@@ -679,12 +651,10 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   // mostly coincide (scene 1's 23 nodes: the union 17 % faster).
   const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= rtwk::kMaxLeafPrims;
   const bool lane = lane_ok && (p->world_traversal == RTW_WORLD_TRAVERSAL_LANE ||
-                                p->world_traversal == RTW_WORLD_TRAVERSAL_LANE_BVH2 ||
                                 (p->world_traversal == RTW_WORLD_TRAVERSAL_AUTO && w->view.n_nodes >= kLaneNodes));
-  // The per-lane walk runs on the 4-wide BVH when the world has one, unless
-  // params.world_traversal asks for the binary one (RTW_WORLD_TRAVERSAL_LANE_BVH2).
-  const bool wide = lane && w->n_nodes4 > 0 && p->world_traversal != RTW_WORLD_TRAVERSAL_LANE_BVH2;
-  c.fs = rtwk::world_feature_set(feat, lane, wide);
+  const char* up = rtw_dev_knob("RTW_WORLD_UNPACKED");  // development knob (A/B): the per-lane walk loads the refs
+  const bool packed = lane && w->packed && !(up && *up == '1');
+  c.fs = rtwk::world_feature_set(feat, lane, packed);
   c.lds = rtwk::world_lds_bytes(w->view.n_perlins, c.fs);
   // Register-allocation target in waves per SIMD (params.world_waves, 0 = the
   // feature set's default).

@@ -34,7 +34,7 @@ DEFAULT_WF_PASSES = 8  # rtw_hip.h RTW_DEFAULT_WF_PASSES (params.wf_passes overr
 WF_DRAIN = {"samples": 0, "slots": 1, "none": 2}  # rtw_wf_drain
 WF_FORM = {"fused": 0, "split": 1}  # rtw_wf_form
 WORLD_FEATURES = {"auto": 0, "all": 1}  # rtw_world_features
-WORLD_TRAVERSAL = {"auto": 0, "union": 1, "lane": 2, "lane2": 3}  # rtw_world_traversal
+WORLD_TRAVERSAL = {"auto": 0, "union": 1, "lane": 2}  # rtw_world_traversal
 STATS_WORDS = 16  # rtw_hip.h RTW_STATS_WORDS
 STAT_NAMES = ["samples", "segments", "f32_skips", "cand_wave_iters", "cand_lanes", "disc_ge0_lanes",
               "sphere_loop_wave_iters", "cull_survivor_lanes", "cull_exact_wave_iters", "drain_segments",

@@ -63,7 +63,7 @@ def test_world_scene1_equals_megakernel(rtw, W, earth):
     assert np.array_equal(mkm.view(np.uint32), wdm.view(np.uint32))
 
 
-TRAVERSALS = ["union", "lane", "lane2"]  # rtw_params.world_traversal: the wave's union walk / per-lane walks (4-wide / binary BVH)
+TRAVERSALS = ["union", "lane"]  # rtw_params.world_traversal: the wave's union walk / per-lane walks
 
 
 @pytest.mark.parametrize("trav", TRAVERSALS)

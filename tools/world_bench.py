@@ -57,7 +57,7 @@ def run(scene, reps=3, spp=None, width=None, linear=False, **pkw):
 
 if __name__ == "__main__":
     # python tools/world_bench.py [scenes] [cfg ...]; cfg = "-" (defaults) or
-    # comma-separated rtw_params fields, e.g. "world_traversal=lane,world_waves=3"
+    # comma-separated rtw_params fields, e.g. "world_traversal=lane,world_waves=3"; WORLD_REPS renders (best of)
     which = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [6, 7, 1, 5, 3, 2, 4]
     cfgs = sys.argv[2:] or ["-"]
     for sc in which:
@@ -66,4 +66,4 @@ if __name__ == "__main__":
             for kv in ([] if cfg == "-" else cfg.split(",")):
                 k, v = kv.split("=")
                 kw[k] = int(v) if v.isdigit() else v
-            print(json.dumps(run(sc, **kw)), flush=True)
+            print(json.dumps(run(sc, reps=int(os.environ.get("WORLD_REPS", "3")), **kw)), flush=True)
