@@ -370,7 +370,6 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
-    (void)pack_refs(bvh, d->n_prims);
     if (flags & RTW_WORLD_DEBUG_BVH) {  // root's two children: leaf (prims) or node, and their boxes
       for (int c = 0; c < 2; ++c) {
         uint32_t ref;
@@ -381,6 +380,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
                 nd[0 + c], nd[6 + c], nd[2 + c], nd[8 + c], nd[4 + c], nd[10 + c]);
       }
     }
+    (void)pack_refs(bvh, d->n_prims);  // (after the diagnostic: it prints the boxes as built)
   } else {
     for (uint32_t i = 0; i < d->n_prims; ++i) bvh.order.push_back(i);
   }
