@@ -514,10 +514,10 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
   // waited for the stack pop's LDS read, which `top` is there to hide)
   using GF = const __attribute__((address_space(1))) float;  // global: vector memory loads, not flat
   GF* nodes = (GF*)W.node;
-  // PACKED: refs in the lower bounds' low bits, as 18 bits (rtw_world_capi.hip pack_refs): a leaf
-  // is LB | (count - 1) << 16 | first; the walk keeps refs in that form (kNoRef stays kNoRef).
+  // PACKED: refs in the lower bounds' low bytes, as 24 bits (rtw_world_capi.hip pack_refs): a leaf
+  // is LB | (count - 1) << 22 | first; the walk keeps refs in that form (kNoRef stays kNoRef).
   constexpr bool PACKED = (FEAT & kFeatPacked) != 0;
-  constexpr uint32_t LB = PACKED ? 0x20000u : kLeafBit;
+  constexpr uint32_t LB = PACKED ? 0x800000u : kLeafBit;
   using GD = const __attribute__((address_space(1))) D;
   GD* pr = (GD*)W.prim;
   asm volatile("" : "+s"(nodes), "+s"(pr));
@@ -570,11 +570,12 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
           hit[c] = n <= f;
         }
         uint32_t r0, r1;
-        if constexpr (PACKED) {  // child c's ref: low 6 bits of its lower x / y / z bounds
-          const uint32_t a0 = __float_as_uint(q0.x), a1 = __float_as_uint(q0.y), b0 = __float_as_uint(q0.z),
-                         b1 = __float_as_uint(q0.w), c0 = __float_as_uint(q1.x), c1 = __float_as_uint(q1.y);
-          r0 = (a0 & 63u) | ((b0 & 63u) << 6) | ((c0 & 63u) << 12);
-          r1 = (a1 & 63u) | ((b1 & 63u) << 6) | ((c1 & 63u) << 12);
+        if constexpr (PACKED) {  // child c's ref: the low bytes of its lower x / y / z bounds
+          // v_perm_b32: byte i of the result = byte sel_i of {S0 (bytes 4-7), S1 (bytes 0-3)}, 0x0C = 0
+          const uint32_t t0 = __builtin_amdgcn_perm(__float_as_uint(q0.z), __float_as_uint(q0.x), 0x0C0C0400u);
+          const uint32_t t1 = __builtin_amdgcn_perm(__float_as_uint(q0.w), __float_as_uint(q0.y), 0x0C0C0400u);
+          r0 = __builtin_amdgcn_perm(__float_as_uint(q1.x), t0, 0x0C040100u);
+          r1 = __builtin_amdgcn_perm(__float_as_uint(q1.y), t1, 0x0C040100u);
         } else {
           const f4 q3 = nd[3];
           r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
@@ -607,8 +608,8 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     if (MODE == 1 && lid == 0) ++wl;
     if (lf != kNoRef) {  // 1 .. kMaxLeafPrims primitives
       static_assert(kWorldRec * sizeof(D) == 128, "primitive record size");
-      const uint32_t first = PACKED ? (lf & 0xFFFFu) : (lf & 0x7FFFFFu);
-      const uint32_t cnt = PACKED ? ((lf >> 16) & 1u) + 1u : (lf >> 23) & kLeafCountMask;
+      const uint32_t first = PACKED ? (lf & 0x3FFFFFu) : (lf & 0x7FFFFFu);
+      const uint32_t cnt = PACKED ? ((lf >> 22) & 1u) + 1u : (lf >> 23) & kLeafCountMask;
       for (uint32_t k = first; k < first + cnt; ++k) {
         if (MODE == 1) ++nt;
         D t;

@@ -101,36 +101,36 @@ struct Bvh {
 };
 
 // The per-lane walk loads a node's 12 bounds (48 B, three 16-B loads) and not
-// its refs (words 12-13): each child's ref, as 18 bits (an interior node
-// index < 2^17, or 0x20000 | (count - 1) << 16 | first primitive < 2^16),
-// rides in the low 6 bits of that child's three lower bounds (words 0 / 2 / 4
-// for child 0, 1 / 3 / 5 for child 1), each moved DOWN to the nearest float
-// whose low bits hold the payload (<= 127 ulps: the box only grows, so the
-// test stays conservative; the union walk reads the same bounds and words
-// 12-13).  The per-lane walk's loads are bound by the vector memory pipeline
+// its refs (words 12-13): each child's ref, as 24 bits (an interior node
+// index < 2^23, or 0x800000 | (count - 1) << 22 | first primitive < 2^22),
+// rides in the low byte of that child's three lower bounds (words 0 / 2 / 4
+// for child 0, 1 / 3 / 5 for child 1; one byte each, gathered by two
+// v_perm_b32), each bound moved DOWN to the nearest float whose low byte is
+// the payload (< 512 ulps: the box only grows, so the test stays
+// conservative; the union walk reads the same bounds and words 12-13).  The per-lane walk's loads are bound by the vector memory pipeline
 // (TD busy ~0.85, profiles/r05/world_ta_pmc.txt): one load of four per visit.
 uint32_t compact_ref(uint32_t r) {
   if (r < rtwk::kLeafBit) return r;
-  return 0x20000u | ((((r >> 23) & rtwk::kLeafCountMask) - 1u) << 16) | (r & 0x7FFFFFu);
+  return 0x800000u | ((((r >> 23) & rtwk::kLeafCountMask) - 1u) << 22) | (r & 0x7FFFFFu);
 }
-float lower_with_low6(float f, uint32_t payload) {  // the largest float <= f whose low 6 bits are `payload`
+float lower_with_low8(float f, uint32_t payload) {  // the largest float <= f whose low byte is `payload`
   uint32_t b;
   std::memcpy(&b, &f, 4);
-  if (!(b & 0x80000000u) && b >= 64u && f != 0.0f) {  // positive: smaller bit patterns are smaller
-    uint32_t c = (b & ~63u) | payload;
-    if (c > b) c -= 64u;
+  if (!(b & 0x80000000u) && b >= 256u && f != 0.0f) {  // positive: smaller bit patterns are smaller
+    uint32_t c = (b & ~255u) | payload;
+    if (c > b) c -= 256u;
     std::memcpy(&f, &c, 4);
     return f;
   }
   const uint32_t m = b & 0x7FFFFFFFu;  // zero, tiny or negative: a larger magnitude below zero
-  uint32_t c = (m & ~63u) | payload;
-  if (c < m) c += 64u;
+  uint32_t c = (m & ~255u) | payload;
+  if (c < m) c += 256u;
   c |= 0x80000000u;
   std::memcpy(&f, &c, 4);
   return f;
 }
 bool pack_refs(Bvh& b, uint32_t n_prims) {
-  if (b.n_nodes >= 0x20000u || n_prims >= 0x10000u || b.max_leaf > 2u) return false;
+  if (b.n_nodes >= 0x800000u || n_prims >= 0x400000u || b.max_leaf > 2u) return false;
   for (uint32_t n = 0; n < b.n_nodes; ++n) {
     float* nd = b.nodes.data() + (size_t)rtwk::kNodeWords * n;
     for (int c = 0; c < 2; ++c) {
@@ -138,7 +138,7 @@ bool pack_refs(Bvh& b, uint32_t n_prims) {
       std::memcpy(&r, nd + 12 + c, 4);
       const uint32_t v = compact_ref(r);
       for (int k = 0; k < 3; ++k) {
-        const float old = nd[2 * k + c], nw = lower_with_low6(old, (v >> (6 * k)) & 63u);
+        const float old = nd[2 * k + c], nw = lower_with_low8(old, (v >> (8 * k)) & 255u);
         if (!(nw <= old) || !std::isfinite(nw)) return false;  // (never: the bounds are finite)
         nd[2 * k + c] = nw;
       }
