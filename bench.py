@@ -766,8 +766,9 @@ def main():
                                                        samples_all, world, rank, dist, tg, torch)
 
     if world == 1 and not args.no_world_variants:
-        extra["globe_10k_variant"] = world_variant(R, torch, 7, max(2, args.steps // 2), 1)
-        extra["cornell_variant"] = world_variant(R, torch, 6, max(2, args.steps // 2), 1)
+        # (at least 10 renders each: one world render varies +-7 % on one box, profiles/r05/world_spread.txt)
+        extra["globe_10k_variant"] = world_variant(R, torch, 7, max(10, args.steps // 2), 2)
+        extra["cornell_variant"] = world_variant(R, torch, 6, max(10, args.steps // 2), 2)
 
     res = {
         "metric": "Msamples/sec (pixels x spp / s), RTIOW cover scene; trace-kernel roofline",
