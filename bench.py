@@ -280,8 +280,9 @@ def world_roofline(scene, s, kernel_ms, info, lane=False):
     measured here; traffic = its PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE.
     With the per-lane BVH walk (lane) the instructions are each lane's own
     path, not the union of the wave's: the line's node visits per segment are
-    per lane (the algorithm's work), and wait_frac shows the remaining bound,
-    the dependent per-lane node loads."""
+    per lane (the algorithm's work), and the vector memory pipeline's busy
+    shares (td_busy_frac_pmc: the per-lane loads' data return) show the other
+    bound the walk runs against."""
     path = evidence(f"world_pmc_{scene}.json")
     trav = "per-lane BVH walks (vector node loads)" if lane else "wave-cooperative BVH traversal (scalar node loads)"
     bound = "valu-issue (" + (trav if info["nodes"] else "wave-uniform scalar-loaded records; linear list, no BVH") + ")"
@@ -299,6 +300,7 @@ def world_roofline(scene, s, kernel_ms, info, lane=False):
             "traffic": round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"]),
             "valu_busy_frac_pmc": t["valu_busy_frac"], "wait_frac_of_wave_cycles": t["wait_frac_of_wave_cycles"],
             "valu_per_wave_iteration": t["valu_per_wave_iteration"], "kernel": "world_kernel",
+            **({"td_busy_frac_pmc": t["td_busy_frac"], "ta_busy_frac_pmc": t["ta_busy_frac"]} if "td_busy_frac" in t else {}),
             "source": os.path.relpath(path, REPO)}
 
 

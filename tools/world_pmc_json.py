@@ -13,9 +13,11 @@ import sys
 
 SIMDS = 256 * 4
 root, scene = sys.argv[1], sys.argv[2]
-c, ms = {}, None
-for tag in "abcfw":
+c, ms, tpass = {}, None, {}
+for tag in "abcfwt":
     d = f"{root}/wpmc_{scene}_{tag}"
+    if tag == "t" and not glob.glob(f"{d}/*counter_collection.csv"):
+        continue  # (older runs: no TA / TD pass)
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for f in glob.glob(f"{d}/*counter_collection.csv"):
@@ -24,6 +26,9 @@ for tag in "abcfw":
                 per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
                 names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
     last = max(per)
+    if tag == "t":  # its own GRBM_GUI_ACTIVE: the busy shares are over this pass's dispatch
+        tpass = dict(per[last])
+        continue
     c.update(per[last])
     if tag == "b":
         for f in glob.glob(f"{d}/*kernel_trace.csv"):
@@ -48,6 +53,11 @@ out = {"what": f"PMC passes of ONE world_kernel dispatch (scene {run['scene']}, 
        "valu_busy_frac": round(c["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc), 4),
        "wait_frac_of_wave_cycles": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4),
        "hbm_fetch_bytes": c["FETCH_SIZE"] * 1024 * 2, "hbm_write_bytes": c["WRITE_SIZE"] * 1024,
+       # vector memory pipeline: TA (address processing, average over instances) and TD (data
+       # return, summed over the 256 CUs' instances) busy cycles over the dispatch's cycles
+       **({"ta_busy_frac": round(tpass["TA_BUSY_avr"] / (tpass["GRBM_GUI_ACTIVE"] / 8), 4),
+           "td_busy_frac": round(tpass["TD_TD_BUSY_sum"] / 256 / (tpass["GRBM_GUI_ACTIVE"] / 8), 4),
+           "vmem_counters": {k: tpass[k] for k in sorted(tpass)}} if tpass else {}),
        "note": "valu_busy_frac = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); a wave64 VALU "
                "instruction occupies its SIMD for ~4 cycles, so the issue roof is 1024 x clock / 4 wave-instructions/s"}
 print(json.dumps(out, indent=1))
