@@ -104,7 +104,7 @@ typedef enum {
 typedef enum {
   RTW_WORLD_TRAVERSAL_AUTO = 0,  /* per lane for sphere worlds of >= 256 BVH nodes, else the union */
   RTW_WORLD_TRAVERSAL_UNION = 1, /* the wave walks the union of its lanes' BVH paths (scalar node loads) */
-  RTW_WORLD_TRAVERSAL_LANE = 2   /* every lane walks its own path (sphere worlds with a BVH of depth <= 24;
+  RTW_WORLD_TRAVERSAL_LANE = 2   /* every lane walks its own path (sphere worlds with a BVH of depth <= 16;
                                     other worlds take the union walk) */
 } rtw_world_traversal;
 
