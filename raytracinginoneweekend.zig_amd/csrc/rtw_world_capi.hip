@@ -129,10 +129,11 @@ float lower_with_low8(float f, uint32_t payload) {  // the largest float <= f wh
   std::memcpy(&f, &c, 4);
   return f;
 }
-bool pack_refs(Bvh& b, uint32_t n_prims) {
+bool pack_refs(Bvh& b, uint32_t n_prims, bool debug) {
   if (b.n_nodes >= 0x800000u || n_prims >= 0x400000u || b.max_leaf > 2u) return false;
+  std::vector<float> packed(b.nodes);
   for (uint32_t n = 0; n < b.n_nodes; ++n) {
-    float* nd = b.nodes.data() + (size_t)rtwk::kNodeWords * n;
+    float* nd = packed.data() + (size_t)rtwk::kNodeWords * n;
     for (int c = 0; c < 2; ++c) {
       uint32_t r;
       std::memcpy(&r, nd + 12 + c, 4);
@@ -144,6 +145,32 @@ bool pack_refs(Bvh& b, uint32_t n_prims) {
       }
     }
   }
+  if (debug) {  // the device's gather (rtw_world.hip trace_phase PACKED) restated, against every ref
+    uint32_t bad = 0, worst = 0;
+    for (uint32_t n = 0; n < b.n_nodes; ++n) {
+      const float* nd = packed.data() + (size_t)rtwk::kNodeWords * n;
+      const float* od = b.nodes.data() + (size_t)rtwk::kNodeWords * n;
+      for (int c = 0; c < 2; ++c) {
+        uint32_t r, w[3], v = 0;
+        std::memcpy(&r, nd + 12 + c, 4);
+        for (int k = 0; k < 3; ++k) {
+          std::memcpy(&w[k], nd + 2 * k + c, 4);
+          v |= (w[k] & 255u) << (8 * k);
+          uint32_t ob;
+          std::memcpy(&ob, od + 2 * k + c, 4);
+          const bool neg = (w[k] | ob) & 0x80000000u;  // ulps between the two (same-sign or across zero)
+          const uint32_t d = neg ? (w[k] & 0x7FFFFFFFu) + ((ob & 0x80000000u) ? 0u - (ob & 0x7FFFFFFFu) : ob)
+                                 : ob - w[k];
+          worst = std::max(worst, d);
+          if (!(nd[2 * k + c] <= od[2 * k + c])) ++bad;
+        }
+        if (v != compact_ref(r)) ++bad;
+      }
+    }
+    fprintf(stderr, "[rtw bvh] packed refs: %u nodes, %u mismatches, bounds moved down by <= %u ulps\n", b.n_nodes,
+            bad, worst);
+  }
+  b.nodes.swap(packed);
   b.packed = true;
   return true;
 }
@@ -380,7 +407,7 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
                 nd[0 + c], nd[6 + c], nd[2 + c], nd[8 + c], nd[4 + c], nd[10 + c]);
       }
     }
-    (void)pack_refs(bvh, d->n_prims);  // (after the diagnostic: it prints the boxes as built)
+    (void)pack_refs(bvh, d->n_prims, (flags & RTW_WORLD_DEBUG_BVH) != 0);  // (after the diagnostic: it prints the boxes as built)
   } else {
     for (uint32_t i = 0; i < d->n_prims; ++i) bvh.order.push_back(i);
   }

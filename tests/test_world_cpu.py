@@ -8,6 +8,7 @@ reference's recursive rayColor (Tier A) on the emissive scenes."""
 import ctypes as C
 import math
 import os
+import re
 import shutil
 import subprocess
 
@@ -327,3 +328,9 @@ def test_globe_bvh_isolates_the_ground_at_the_root():
     assert len(lines) == 2, p.stderr
     assert "leaf of 1, box x [-1000, 1000] y [-2000, 0] z [-1000, 1000]" in lines[0]
     assert "node" in lines[1] and "y [0, 4]" in lines[1]
+    # the per-lane walk's refs packed into the lower bounds (rtw_world_capi.hip pack_refs): the
+    # device's byte gather restated on the host recovers every ref, and no bound moved up
+    packed = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh] packed refs:")]
+    assert len(packed) == 1, p.stderr
+    m = re.match(r"\[rtw bvh\] packed refs: (\d+) nodes, (\d+) mismatches, bounds moved down by <= (\d+) ulps", packed[0])
+    assert m and int(m.group(1)) > 5000 and int(m.group(2)) == 0 and int(m.group(3)) < 512, packed[0]
