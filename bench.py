@@ -406,6 +406,16 @@ def wavefront_bytes(counts, precision, units, fused=True, bounces=1):
     return queued * seg // max(1, bounces) + counts["samples"] * (2 * (24 + 4) + 4) + units * 24
 
 
+def wf_frame_bytes(args, counts, units):
+    """wavefront_bytes of a frame rendered with args' engine configuration: the
+    fused form crosses the queues once per args.wf_bounces segments, the split
+    form once per segment.  The one call both wavefront rooflines (the headline
+    with --engine wavefront and the wavefront_variant line) make, so they agree
+    (the headline passed no bounce count)."""
+    fused = args.wf_form == "fused"
+    return wavefront_bytes(counts, args.precision, units, fused, (args.wf_bounces or 1) if fused else 1)
+
+
 def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, samples_all, world, rank, dist,
                       tg, torch):
     """configs[3]: the same frame on the wavefront engine (bit-identical image,
@@ -439,8 +449,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
     sclk = clk.mhz()
     chunk = min(R.DEFAULT_CHUNK, spp)
     units = rc * W * ((spp + chunk - 1) // chunk)
-    kb = args.wf_bounces or 1
-    byts = wavefront_bytes(counts, args.precision, units, args.wf_form == "fused", kb if args.wf_form == "fused" else 1)
+    byts = wf_frame_bytes(args, counts, units)
     gbs = byts / (ms * 1e-3) / 1e9
     drain = counts.get("drain_segments", 0) / max(1, counts["segments"])
     # The same frame with 2 and 3 bounce segments per wf_step launch
@@ -478,7 +487,7 @@ def wavefront_variant(args, R, rend, cam, out, W, H, spp, rb, rs, rc, counts, sa
                              "algorithmic_bytes_per_frame": bk}
     return {"value": round(samples_all * args.steps / e / 1e6, 2), "ms_per_step": round(e / args.steps * 1e3, 3),
             "wf_paths": args.wf_paths or R.DEFAULT_WF_PATHS, "wf_sets": wf_sets(args), "wf_drain": args.wf_drain,
-            "wf_form": args.wf_form, "wf_bounces": kb,
+            "wf_form": args.wf_form, "wf_bounces": args.wf_bounces or 1,
             "wf_passes": wf_passes(args) if args.wf_form == "fused" else 1, "sclk_mhz": sclk, "sclk_window_ms": clk.window_ms,
             "bounces_per_launch": sweep,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -725,7 +734,7 @@ def main():
                     "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
         }
     else:  # wavefront headline: HBM-bound path queues
-        byts = wavefront_bytes(rend.counts(cam, params), args.precision, rc * W * n_chunks, args.wf_form == "fused")
+        byts = wf_frame_bytes(args, rend.counts(cam, params), rc * W * n_chunks)
         gbs = byts / (trace_ms_avg * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": wf_traffic(args, W, rc, spp),

@@ -104,8 +104,10 @@ typedef enum {
 typedef enum {
   RTW_WORLD_TRAVERSAL_AUTO = 0,  /* per lane for sphere worlds of >= 256 BVH nodes, else the union */
   RTW_WORLD_TRAVERSAL_UNION = 1, /* the wave walks the union of its lanes' BVH paths (scalar node loads) */
-  RTW_WORLD_TRAVERSAL_LANE = 2   /* every lane walks its own path (sphere worlds with a BVH of depth <= 16;
+  RTW_WORLD_TRAVERSAL_LANE = 2,  /* every lane walks its own path (sphere worlds with a BVH of depth <= 16 —
+                                    rtw_world_create caps the depth of large sphere worlds' trees at 16 —
                                     other worlds take the union walk) */
+  RTW_WORLD_TRAVERSAL_LINEAR = 3 /* (reported only, rtw_world_launch_info: a world without a BVH) */
 } rtw_world_traversal;
 
 typedef struct {
@@ -128,8 +130,9 @@ typedef struct {
   uint32_t wf_sets;           /* wavefront: independent queue sets (1-4), 0 = RTW_DEFAULT_WF_SETS */
   uint32_t wf_drain;          /* wavefront: rtw_wf_drain */
   uint32_t wf_form;           /* wavefront: rtw_wf_form */
-  uint32_t world_waves;       /* world kernel: register budget in waves per SIMD (1, 3 or 4),
-                                 0 = the feature set's default (4 sphere worlds, 3 rects / transforms, 2 noise) */
+  uint32_t world_waves;       /* world kernel: register budget in waves per SIMD: 3 or 4, or 1 = unconstrained
+                                 (any other value fails with RTW_EINVAL); 0 = the feature set's default
+                                 (4 sphere worlds, 3 rects / transforms, 1 noise textures) */
   uint32_t world_features;    /* world kernel: rtw_world_features */
   uint32_t world_traversal;   /* world kernel: rtw_world_traversal */
   uint32_t wf_bounces;        /* wavefront: bounce segments per path per wf_step launch (the path stays in
@@ -363,6 +366,13 @@ int rtw_world_render_device(rtw_world world, const rtw_camera *cam, const rtw_pa
 /* Synchronous host-buffer render of a world description. */
 int rtw_world_render(const rtw_camera *cam, const rtw_world_desc *desc, const rtw_params *params,
                      uint8_t *rgb_out, float *mean_out);
+/* How a render of `world` with `params` would launch on the current device
+ * (the world's): info_out[6] = {traversal (rtw_world_traversal: LANE, UNION
+ * or LINEAR, after AUTO and the world's limits are applied), kernel feature
+ * set, register budget (waves per SIMD: 4, 3, or 1 = unconstrained),
+ * workgroups per CU, persistent grid (workgroups), dynamic LDS bytes per
+ * workgroup}. */
+int rtw_world_launch_info(rtw_world world, const rtw_params *params, uint32_t info_out[6]);
 /* Statistics pass: counts_out[4] = {samples, segments, node_visits, prim_tests}. */
 int rtw_world_render_counts(rtw_world world, const rtw_camera *cam, const rtw_params *params,
                             void *workspace, size_t workspace_bytes, uint64_t counts_out[4]);

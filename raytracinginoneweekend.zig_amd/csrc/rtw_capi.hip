@@ -514,7 +514,8 @@ int validate(const rtw_params* p) {
   if (p->wf_sets > RTW_MAX_WF_SETS) return fail(RTW_EINVAL, "wf_sets %u outside [0, %u]", p->wf_sets, RTW_MAX_WF_SETS);
   if (p->wf_drain > RTW_WF_DRAIN_NONE) return fail(RTW_EINVAL, "wf_drain %u", p->wf_drain);
   if (p->wf_form > RTW_WF_SPLIT) return fail(RTW_EINVAL, "wf_form %u", p->wf_form);
-  if (p->world_waves > 4) return fail(RTW_EINVAL, "world_waves %u outside [0, 4]", p->world_waves);
+  if (p->world_waves > 4 || p->world_waves == 2)  // (compiled budgets: 1 = unconstrained, 3, 4)
+    return fail(RTW_EINVAL, "world_waves %u is not 0, 1, 3 or 4", p->world_waves);
   if (p->world_features > RTW_WORLD_FEATURES_ALL) return fail(RTW_EINVAL, "world_features %u", p->world_features);
   if (p->world_traversal > RTW_WORLD_TRAVERSAL_LANE) return fail(RTW_EINVAL, "world_traversal %u", p->world_traversal);
   if (p->wf_bounces > 16) return fail(RTW_EINVAL, "wf_bounces %u outside [0, 16]", p->wf_bounces);
@@ -753,18 +754,19 @@ uint32_t* poll_words() {
 // thread, so a process does not accumulate streams beyond the hardware
 // queues, where HIP would map them round-robin onto shared queues and a set
 // could land on its caller's queue — correct, but serial); non-blocking,
-// joined to the caller's stream by events on every render; destroyed at
-// library teardown.  Concurrent wavefront renders on one device from several
+// joined to the caller's stream by events on every render; kept for the
+// life of the process.  Concurrent wavefront renders on one device from several
 // threads share them (stream-ordered: still correct).
+// The streams live for the process and are never destroyed: a
+// static destructor would run during exit, possibly after the HIP runtime's
+// own teardown (registered at the first HIP call, after this object was
+// constructed), where hipStreamDestroy may crash or hang.  The runtime
+// releases them with the process.
 struct SideStreams {
   std::mutex mu;
   std::map<std::pair<int, uint32_t>, hipStream_t> s;
-  ~SideStreams() {
-    for (auto& kv : s)
-      if (kv.second) (void)hipStreamDestroy(kv.second);
-  }
 };
-SideStreams g_side;
+SideStreams& g_side = *new SideStreams;  // (leaked on purpose: no exit-time destructor)
 hipStream_t wf_side_stream(int dev, uint32_t k) {
   std::lock_guard<std::mutex> lk(g_side.mu);
   hipStream_t& s = g_side.s[{dev, k}];

@@ -251,6 +251,9 @@ constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder c
 // a BVH of depth <= kLaneStack never overflows it (a push per level at most);
 // deeper BVHs take the union walk
 constexpr uint32_t kLaneStack = 16;
+// per-lane walk: a paused walk keeps its closest hit's stored position + 1 in
+// the low kTravPosBits of one LDS word (rtw_world.hip LaneTravRows)
+constexpr uint32_t kTravPosBits = 26;
 #ifndef RTW_MAX_LEAF_PRIMS
 #define RTW_MAX_LEAF_PRIMS 2  // BVH leaf size (profiles/r01/world_leaf_ab.txt; experiment builds override it)
 #endif

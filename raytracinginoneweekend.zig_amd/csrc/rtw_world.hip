@@ -213,6 +213,17 @@ __device__ __forceinline__ float min_q(float a, float b) {
   return r;
 }
 
+__device__ __forceinline__ float max3_q(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float min3_q(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // The adjacent f32 toward +inf / -inf (finite or infinite x; NaN kept).
 __device__ __forceinline__ float next_up(float x) {
   if (!(x < __builtin_inff())) return x;
@@ -221,6 +232,23 @@ __device__ __forceinline__ float next_up(float x) {
   return __uint_as_float(x > 0.0f ? b + 1u : b - 1u);
 }
 __device__ __forceinline__ float next_down(float x) { return -next_up(-x); }
+
+// a * {p[SP], p[SP]} + {q[SQ], q[SQ]} as one v_pk_fma_f32: op_sel / op_sel_hi
+// pick the 32-bit half of each 64-bit operand for the low / high result, so
+// two broadcast operands share one register pair (bc() pairs hold one value twice).
+template <int SP, int SQ>
+__device__ __forceinline__ f2 pk_fma_sel(f2 a, f2 p, f2 q) {
+  f2 r;
+  if constexpr (SP == 0 && SQ == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(p), "v"(q));
+  else if constexpr (SP == 1 && SQ == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(a), "v"(p), "v"(q));
+  else if constexpr (SP == 0 && SQ == 1)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(p), "v"(q));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(p), "v"(q));
+  return r;
+}
 
 struct WHit {
   int pos;     // stored position of the winner (-1: miss)
@@ -459,23 +487,31 @@ __device__ __forceinline__ void closest(const WV& W, D m, uint32_t* stack, const
 // start their next segments (dynamic ray fetch).  No result depends on when a
 // walk pauses.
 constexpr uint32_t kNoRef = 0xFFFFFFFFu;  // (never a ref: interior refs < kLeafBit, leaf counts <= 2)
-constexpr uint32_t kTravWords = 10;       // LaneTrav rows: ref, pend, top, sp, tmaxf, pos, orig, nan, t (2)
+// LaneTrav rows, [field][lane]: ref, pend, top; (pos + 1) | sp << 26 | nan << 31;
+// orig; t (2 words).  The walk's f32 bound tmaxf is round_up(t), remade on
+// resume.  (7 words: with the lane's attenuation rows, the per-lane kernel's
+// LDS is 40 KB per 4-wave workgroup, four per CU: world_lds_bytes.)
+constexpr uint32_t kTravWords = 7;
 struct LaneTravRows {                     // one wave's rows, [field][lane]
   uint32_t w[kTravWords][64];
 };
+// A wave's dynamic LDS in the per-lane kernel, in 32-bit words: the stack
+// columns, the LaneTrav rows and the attenuation rows (3 f64 per lane).  With
+// the static tail rows (5 words per lane) and chunk sums (3 f64) a 4-wave
+// workgroup holds 40 KB: four fit the CU's 160 KB (4 waves per SIMD).
+constexpr uint32_t kLaneWaveWords = (kLaneStack + kTravWords + 6u) * 64u;
+static_assert((kLaneWaveWords + (5u + 6u) * 64u) * 4u * (kWorldBlock / 64) * 4u <= 160u * 1024u,
+              "per-lane kernel: four 4-wave workgroups per CU");
 // Starts a walk from the root for this lane (no hit yet).
 __device__ __forceinline__ void trav_begin(LaneTravRows* R, uint32_t lid) {
   R->w[0][lid] = 0u;  // the root node
   R->w[1][lid] = kNoRef;
   R->w[2][lid] = kNoRef;
-  R->w[3][lid] = 0u;
-  R->w[4][lid] = __float_as_uint(__builtin_inff());
-  R->w[5][lid] = 0xFFFFFFFFu;  // pos -1
-  R->w[6][lid] = 0xFFFFFFFFu;  // orig -1
-  R->w[7][lid] = 0u;
+  R->w[3][lid] = 0u;           // pos -1, sp 0, no NaN
+  R->w[4][lid] = 0xFFFFFFFFu;  // orig -1
   const uint64_t tb = __builtin_bit_cast(uint64_t, (D)__builtin_huge_val());
-  R->w[8][lid] = (uint32_t)tb;
-  R->w[9][lid] = (uint32_t)(tb >> 32);
+  R->w[5][lid] = (uint32_t)tb;
+  R->w[6][lid] = (uint32_t)(tb >> 32);
 }
 // One traversal phase of the lanes with `walking` set; returns true for the
 // lanes whose walk finished in it (`h` = the closest hit).  Wave-converged.
@@ -485,30 +521,38 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
                                            WHit& h, unsigned long long& nv, unsigned long long& nt,
                                            unsigned long long& wi, unsigned long long& wl) {
   if (!wany(walking)) return false;
+  auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
   uint32_t ref = kNoRef, pend = kNoRef, top = kNoRef, sp = 0u;
   float tmaxf = 0.0f;
   if (walking) {
     ref = R->w[0][lid];
     pend = R->w[1][lid];
     top = R->w[2][lid];
-    sp = R->w[3][lid];
-    tmaxf = __uint_as_float(R->w[4][lid]);
-    h.pos = (int)R->w[5][lid];
-    h.orig = (int)R->w[6][lid];
-    h.nan = R->w[7][lid];
-    h.t = __builtin_bit_cast(D, (uint64_t)R->w[8][lid] | ((uint64_t)R->w[9][lid] << 32));
+    const uint32_t w3 = R->w[3][lid];
+    h.pos = (int)(w3 & ((1u << kTravPosBits) - 1u)) - 1;
+    sp = (w3 >> kTravPosBits) & 31u;
+    h.nan = w3 >> 31;
+    h.orig = (int)R->w[4][lid];
+    h.t = __builtin_bit_cast(D, (uint64_t)R->w[5][lid] | ((uint64_t)R->w[6][lid] << 32));
+    tmaxf = round_up(h.t);  // (the walk keeps tmaxf == round_up(h.t): at its start, after every leaf)
   }
   const V inv = mk((D)1 / d.x, (D)1 / d.y, (D)1 / d.z);
-  const f2 ix = bc((float)inv.x), iy = bc((float)inv.y), iz = bc((float)inv.z);
+  // The union walk's slab constants (closest), held two to a 64-bit register
+  // pair instead of one value twice (bc): the per-lane walk's node bounds are
+  // VGPRs, so its v_pk_fma_f32 broadcasts each constant from the half of the
+  // pair op_sel names (pk_fma_sel) — 9 VGPRs fewer across the walk, which at the
+  // 4-wave budget (128 VGPRs) is what kept the loop off scratch (the globe's
+  // per-lane kernel spilled 80 B/lane, rewritten in its loop: DESIGN.md §6.3).
+  const float ixf = (float)inv.x, iyf = (float)inv.y, izf = (float)inv.z;
   const float mf = (float)m;
-  const float pxo = -(float)o.x * ix[0], pyo = -(float)o.y * iy[0], pzo = -(float)o.z * iz[0];
-  const float mx = mf * fabsf(ix[0]), my = mf * fabsf(iy[0]), mz = mf * fabsf(iz[0]);
-  const float sx = ix[0] < 0.0f ? -1.0f : 1.0f, sy = iy[0] < 0.0f ? -1.0f : 1.0f, sz = iz[0] < 0.0f ? -1.0f : 1.0f;
-  const f2 oxl = bc(pxo - sx * mx), oxh = bc(pxo + sx * mx);
-  const f2 oyl = bc(pyo - sy * my), oyh = bc(pyo + sy * my);
-  const f2 ozl = bc(pzo - sz * mz), ozh = bc(pzo + sz * mz);
+  const float pxo = -(float)o.x * ixf, pyo = -(float)o.y * iyf, pzo = -(float)o.z * izf;
+  const float mx = mf * fabsf(ixf), my = mf * fabsf(iyf), mz = mf * fabsf(izf);
+  const float sx = ixf < 0.0f ? -1.0f : 1.0f, sy = iyf < 0.0f ? -1.0f : 1.0f, sz = izf < 0.0f ? -1.0f : 1.0f;
   const float tminf = next_down((float)tmin);
-  auto round_up = [](D x) { return (D)(float)x < x ? next_up((float)x) : (float)x; };
+  const f2 I1 = f2{ixf, iyf}, I2 = f2{izf, tminf};
+  const f2 O1 = f2{pxo - sx * mx, pyo - sy * my};  // lower x, y offsets
+  const f2 O2 = f2{pzo - sz * mz, pxo + sx * mx};  // lower z, upper x
+  const f2 O3 = f2{pyo + sy * my, pzo + sz * mz};  // upper y, z
   // the node and primitive tables' addresses, read from the kernel argument
   // once per phase (re-read in the loop, the scalar load's lgkmcnt wait also
   // waited for the stack pop's LDS read, which `top` is there to hide)
@@ -556,16 +600,19 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
         const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
             reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 6));
         const f4 q0 = nd[0], q1 = nd[1], q2 = nd[2];
-        // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3, refs in words 12-13
-        const f2 x0 = pfma(f2{q0.x, q0.y}, ix, oxl), x1 = pfma(f2{q1.z, q1.w}, ix, oxh);
-        const f2 y0 = pfma(f2{q0.z, q0.w}, iy, oyl), y1 = pfma(f2{q2.x, q2.y}, iy, oyh);
-        const f2 z0 = pfma(f2{q1.x, q1.y}, iz, ozl), z1 = pfma(f2{q2.z, q2.w}, iz, ozh);
+        // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3 (refs in words 12-13);
+        // the per-lane constants two to a register pair (pk_fma_sel)
+        const f2 x0 = pk_fma_sel<0, 0>(f2{q0.x, q0.y}, I1, O1), x1 = pk_fma_sel<0, 1>(f2{q1.z, q1.w}, I1, O2);
+        const f2 y0 = pk_fma_sel<1, 1>(f2{q0.z, q0.w}, I1, O1), y1 = pk_fma_sel<1, 0>(f2{q2.x, q2.y}, I1, O3);
+        const f2 z0 = pk_fma_sel<0, 0>(f2{q1.x, q1.y}, I2, O2), z1 = pk_fma_sel<0, 1>(f2{q2.z, q2.w}, I2, O3);
         float tn[2];
         bool hit[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          const float n = fmaxf(fmaxf(fminf(x0[c], x1[c]), fminf(y0[c], y1[c])), max_q(fminf(z0[c], z1[c]), tminf));
-          const float f = fminf(fminf(fmaxf(x0[c], x1[c]), fmaxf(y0[c], y1[c])), min_q(fmaxf(z0[c], z1[c]), tmaxf));
+          // (all in asm: the compiler would re-quiet the asm FMAs' outputs before each fminf / fmaxf,
+          // but an FMA returns quiet NaNs only, so v_min / v_max on them are fminf / fmaxf)
+          const float n = max3_q(min_q(x0[c], x1[c]), min_q(y0[c], y1[c]), max_q(min_q(z0[c], z1[c]), I2[1]));
+          const float f = min3_q(max_q(x0[c], x1[c]), max_q(y0[c], y1[c]), min_q(max_q(z0[c], z1[c]), tmaxf));
           tn[c] = n;
           hit[c] = n <= f;
         }
@@ -625,14 +672,11 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
     R->w[0][lid] = ref;
     R->w[1][lid] = pend;
     R->w[2][lid] = top;
-    R->w[3][lid] = sp;
-    R->w[4][lid] = __float_as_uint(tmaxf);
-    R->w[5][lid] = (uint32_t)h.pos;
-    R->w[6][lid] = (uint32_t)h.orig;
-    R->w[7][lid] = h.nan;
+    R->w[3][lid] = (uint32_t)(h.pos + 1) | (sp << kTravPosBits) | (h.nan << 31);
+    R->w[4][lid] = (uint32_t)h.orig;
     const uint64_t tb = __builtin_bit_cast(uint64_t, h.t);
-    R->w[8][lid] = (uint32_t)tb;
-    R->w[9][lid] = (uint32_t)(tb >> 32);
+    R->w[5][lid] = (uint32_t)tb;
+    R->w[6][lid] = (uint32_t)(tb >> 32);
   }
   return finished;
 }
@@ -706,22 +750,24 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   // this wave's BVH stack: one column per lane (per-lane traversal) or one
   // wave-uniform stack (the union walk)
   uint32_t* stack = reinterpret_cast<uint32_t*>(lds_raw) +
-                    (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? (kLaneStack + kTravWords) * 64u : kBvhStack);
-  // per-lane traversal: this wave's LaneTrav rows follow its stack columns
+                    (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? kLaneWaveWords : kBvhStack);
+  // per-lane traversal: this wave's LaneTrav rows follow its stack columns,
+  // and the lanes' attenuation rows (T) follow them
   LaneTravRows* trav_rows = reinterpret_cast<LaneTravRows*>(stack + kLaneStack * 64u);
+  double(*t_rows)[64] = reinterpret_cast<double(*)[64]>(stack + (kLaneStack + kTravWords) * 64u);
   // Tail dealing rows of this wave's lanes (lane = the owner of a unit): the
   // first sample handed to other lanes (samples [hi, s_end) are theirs), the
   // ring entries they filled, the unit's pixel; and the dealing list.
   // (Row addresses formed at each use from the wave-uniform index: held as
   // pointers they cost registers across the whole loop.)
-  __shared__ uint32_t tail_rows[kWorldBlock / 64][6][64];
+  __shared__ uint32_t tail_rows[kWorldBlock / 64][5][64];
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #define TL_HI tail_rows[wv][0]
 #define TL_READY tail_rows[wv][1]
 #define TL_PXLY tail_rows[wv][2]
 #define TL_LIST tail_rows[wv][3]
 #define TL_OWN tail_rows[wv][4]  // a helper's owner lane
-#define TL_C tail_rows[wv][5]    // the unit's chunk
+#define TL_C tail_rows[wv][4]    // an owner's chunk (one row: a lane helps only once it owns no unit)
   // The lane's f64 chunk sum (a helper's: the radiance of the sample it
   // traces) lives in LDS too: it changes only when a sample ends.
   __shared__ double home_sum[kWorldBlock / 64][3][64];
@@ -745,6 +791,21 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
   L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
   L.rs = 0;
   L.skip = -1;
+  // The path attenuation T (rayColor's product of attenuations, main.zig:117)
+  // of the per-lane kernel lives in LDS rows: it changes only when a segment
+  // is shaded, and held in VGPRs across the BVH walk it was what the 4-wave
+  // budget spilled (written back every iteration of the persistent loop).
+  auto t_get = [&]() -> V {
+    if constexpr ((FEAT & kFeatLane) != 0) return mk(t_rows[0][lid], t_rows[1][lid], t_rows[2][lid]);
+    return L.T;
+  };
+  auto t_set = [&](const V& v) {
+    if constexpr ((FEAT & kFeatLane) != 0) {
+      t_rows[0][lid] = v.x, t_rows[1][lid] = v.y, t_rows[2][lid] = v.z;
+    } else {
+      L.T = v;
+    }
+  };
   // rayColor forward (main.zig:103-122): a sample's radiance is nonzero only at
   // the event that ends it (a miss adds T * background, a light T * emitted),
   // so that one term joins the chunk sum directly: sx + (0 + x) == sx + x
@@ -872,6 +933,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         if (in_unit_ball<D, 2>(dk)) break;
       }
       start_sample_ray<D>(kargs<D>(), L, u, v, dk[0], dk[1]);
+      t_set(L.T);  // (= 1, 1, 1: start_sample_ray)
       have_ray = true;
     }
     // ---- one segment ----
@@ -881,7 +943,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
     auto shade = [&](WHit& h) {
       if (__builtin_expect(h.nan != 0u, 0)) seq_hit<FEAT>(W, order, L.o, L.d, L.time, WKA(t.tmin), h);
       if (h.pos < 0) {  // miss: background (main.zig:109-112)
-        const V c = mulv(L.T, ld3(opaque(kargs<D>())->bg));
+        const V c = mulv(t_get(), ld3(opaque(kargs<D>())->bg));
         HS(0) += c.x;
         HS(1) += c.y;
         HS(2) += c.z;
@@ -930,7 +992,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         }
         if ((FEAT & kFeatXform) && xf >= 0) to_world(W.xform + kWorldRec * xf, p, nrm);
         if (mkind == 3u) {  // DiffuseLight: emitted, no scatter (material.zig:94-110)
-          const V c = mulv(L.T, tex_value<FEAT>(W, mtex, tu, tv, p));
+          const V c = mulv(t_get(), tex_value<FEAT>(W, mtex, tu, tv, p));
           HS(0) += c.x;
           HS(1) += c.y;
           HS(2) += c.z;
@@ -991,7 +1053,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
           if (absorbed) {
             ended = true;
           } else {
-            L.T = mulv(L.T, att);
+            t_set(mulv(t_get(), att));
             L.o = p;
             L.d = ndir;
             L.depth++;
@@ -1010,8 +1072,12 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
         }
       }
       WSTAMP(1)  // sample start (+ take units, loop control)
-      // once every lane's unit queue ran dry, walks run to their end (no yield)
-      const uint32_t yl = wall(done) ? 0u : WKA(lane_yield);
+      // (walks yield in the tail copy of the loop too: the lanes that stopped
+      // walking then take the wave's other units' samples.  A `wall(done)` test
+      // here never held while a lane walked — a done lane without a unit only
+      // walks as a helper, and helpers exist only while an owner, not done,
+      // holds its unit: ADVICE r5 — and is gone.)
+      const uint32_t yl = WKA(lane_yield);
       WHit h;
       if (trav_phase<MODE, FEAT>(W, WKA(margin), stack, trav_rows, lid, walking, yl, L.o, L.d, L.time, WKA(t.tmin),
                                  h, n_visits, n_tests, n_wi, n_wl)) {
@@ -1122,8 +1188,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 }
 
 size_t world_lds_bytes(uint32_t, int fs) {
-  return (size_t)((fs & kFeatLane) ? (kLaneStack + kTravWords) * 64u : kBvhStack) * (kWorldBlock / 64) *
-         sizeof(uint32_t);
+  return (size_t)((fs & kFeatLane) ? kLaneWaveWords : kBvhStack) * (kWorldBlock / 64) * sizeof(uint32_t);
 }
 
 template <int OCC, int FEAT>
@@ -1141,12 +1206,16 @@ static void launch_occ(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_
 }
 template <int FEAT>
 static void launch_feat(const WorldArgs& a, uint32_t grid, size_t lds, hipStream_t s, int mode, int occ) {
+#ifdef RTW_WORLD_ISA_QUICK  // (ISA inspection of the globe's kernel only: tools/isa_world.sh)
+  if constexpr (FEAT == (kFeatImage | kFeatLane | kFeatPacked)) hipLaunchKernelGGL((world_kernel<0, 4, FEAT>), dim3(grid), dim3(kWorldBlock), lds, s, a);
+#else
   if (occ >= 4)
     launch_occ<4, FEAT>(a, grid, lds, s, mode);
   else if (occ == 3)
     launch_occ<3, FEAT>(a, grid, lds, s, mode);
   else
     launch_occ<1, FEAT>(a, grid, lds, s, mode);
+#endif
 }
 // Instantiated feature sets: spheres with solid / checker / image textures
 // (scenes 1, 2, 4 and configs[4]'s globe), rects + transforms + lights without
@@ -1175,12 +1244,16 @@ template <int FEAT>
 static int bpc_feat(size_t lds, int occ) {
   int nb = 0;
   hipError_t e;
+#ifdef RTW_WORLD_ISA_QUICK
+  e = hipSuccess, nb = 1, (void)lds, (void)occ;
+#else
   if (occ >= 4)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 4, FEAT>, kWorldBlock, lds);
   else if (occ == 3)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 3, FEAT>, kWorldBlock, lds);
   else
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, world_kernel<0, 1, FEAT>, kWorldBlock, lds);
+#endif
   return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 int world_blocks_per_cu(size_t lds, int occ, int fs) {

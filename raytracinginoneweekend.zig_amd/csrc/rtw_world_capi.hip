@@ -186,8 +186,13 @@ constexpr size_t kLeafOneMin = 512;
 
 class Builder {
  public:
-  Builder(const std::vector<Box>& boxes, Bvh& out)
-      : boxes_(boxes), out_(out), leaf_max_(boxes.size() >= kLeafOneMin ? 1u : rtwk::kMaxLeafPrims) {
+  // depth_cap: the tree's depth (interior levels on a root-to-leaf path) stays
+  // <= depth_cap - 1 for the union walk's kBvhStack and <= depth_cap for
+  // depth_cap = kLaneStack (the per-lane walk's rebuild, below): SAH splits
+  // while a median subtree of the rest still fits, median splits after that.
+  Builder(const std::vector<Box>& boxes, Bvh& out, uint32_t depth_cap = rtwk::kBvhStack)
+      : boxes_(boxes), out_(out), leaf_max_(boxes.size() >= kLeafOneMin ? 1u : rtwk::kMaxLeafPrims),
+        cap_(depth_cap), lane_cap_(depth_cap != rtwk::kBvhStack) {
     idx_.resize(boxes.size());
     for (size_t i = 0; i < idx_.size(); ++i) idx_[i] = (uint32_t)i;
     for (const Box& b : boxes) {
@@ -206,6 +211,8 @@ class Builder {
   const std::vector<Box>& boxes_;
   Bvh& out_;
   const uint32_t leaf_max_;  // primitives per leaf (<= rtwk::kMaxLeafPrims)
+  const uint32_t cap_;       // depth cap (see the constructor)
+  const bool lane_cap_;      // the per-lane walk's cap: SAH while depth + need < cap (else + 2 < cap)
   std::vector<uint32_t> idx_;
   std::vector<std::array<double, 3>> cent_;
 
@@ -280,7 +287,7 @@ class Builder {
   uint32_t child(uint32_t b, uint32_t e, uint32_t depth) {
     // Leaves: few primitives, or the depth cap of the per-lane LDS stack
     // (node() switches to median splits while they still fit the cap).
-    if (e - b <= leaf_max_ || (depth >= rtwk::kBvhStack - 1 && e - b <= rtwk::kLeafCountMask))
+    if (e - b <= leaf_max_ || (depth >= (lane_cap_ ? cap_ : cap_ - 1) && e - b <= rtwk::kLeafCountMask))
       return leaf(b, e);
     const uint32_t n = alloc();
     node(n, b, e, depth);
@@ -295,7 +302,7 @@ class Builder {
       // SAH while the median-split depth of the rest still fits the stack.
       uint32_t need = 0;
       for (uint32_t c = e - b; c > leaf_max_; c = (c + 1) / 2) ++need;
-      m = split(b, e, depth + need + 2 < rtwk::kBvhStack);
+      m = split(b, e, lane_cap_ ? depth + need < cap_ : depth + need + 2 < cap_);
     }
     // Child 0 is built first, so an interior child 0 is record n + 1, the line
     // the traversal loads with node n (rtw_world.hip RTW_WORLD_TOUCH_NEXT).
@@ -397,6 +404,20 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
   const bool use_bvh = !(flags & RTW_WORLD_LINEAR) && d->n_prims > kLinearMax;
   if (use_bvh) {
     Builder(boxes, bvh).run();
+    // The per-lane walk (sphere worlds of >= kLeafOneMin primitives, leaves
+    // of one) keeps its stack in kLaneStack LDS entries per lane: a tree
+    // deeper than that is rebuilt with SAH splits only while a median subtree
+    // of the rest still fits (depth <= kLaneStack), so the lane walk stays
+    // available; the globe's SAH tree (depth 16) is already within it.
+    const uint32_t unconstrained_depth = bvh.max_depth;
+    if (bvh.max_leaf == 1 && bvh.max_depth > rtwk::kLaneStack) {
+      Bvh capped;
+      Builder(boxes, capped, rtwk::kLaneStack).run();
+      if (capped.max_depth <= rtwk::kLaneStack && capped.max_leaf == 1) bvh = std::move(capped);
+    }
+    if (flags & RTW_WORLD_DEBUG_BVH)
+      fprintf(stderr, "[rtw bvh] %u nodes, depth %u (unconstrained SAH: %u), max leaf %u\n", bvh.n_nodes,
+              bvh.max_depth, unconstrained_depth, bvh.max_leaf);
     if (flags & RTW_WORLD_DEBUG_BVH) {  // root's two children: leaf (prims) or node, and their boxes
       for (int c = 0; c < 2; ++c) {
         uint32_t ref;
@@ -659,7 +680,7 @@ double bvh_margin(const rtw_world_s* w, const rtw_camera* cam) {
 // common region (rtw_ws_total), so renders on different streams with their
 // own workspaces never share one.
 struct WorldLaunchCfg {
-  int fs, oi;
+  int fs, oi, bpc;
   size_t lds;
   uint32_t grid;
   size_t ring_off, ring_bytes;  // ring: [ring_off, ring_off + ring_bytes) of the workspace
@@ -676,7 +697,8 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
   // AUTO: per lane on BVHs of >= kLaneNodes nodes (configs[4]'s globe: 5,802
   // nodes, +30 %); the union walk on small trees, where the lanes' paths
   // mostly coincide (scene 1's 23 nodes: the union 17 % faster).
-  const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= rtwk::kMaxLeafPrims;
+  const bool lane_ok = w->view.n_nodes > 0 && w->info[2] <= rtwk::kLaneStack && w->info[3] <= rtwk::kMaxLeafPrims &&
+                       w->view.n_prims + 1u < (1u << rtwk::kTravPosBits);
   const bool lane = lane_ok && (p->world_traversal == RTW_WORLD_TRAVERSAL_LANE ||
                                 (p->world_traversal == RTW_WORLD_TRAVERSAL_AUTO && w->view.n_nodes >= kLaneNodes));
   const char* up = rtw_dev_knob("RTW_WORLD_UNPACKED");  // development knob (A/B): the per-lane walk loads the refs
@@ -697,6 +719,7 @@ WorldLaunchCfg world_cfg(const rtw_world_s* w, const rtw_params* p, int dev) {
       bpc_cache[c.fs][c.oi] = rtwk::world_blocks_per_cu(c.lds, c.oi, c.fs), bpc_lds[c.fs][c.oi] = c.lds;
     bpc = bpc_cache[c.fs][c.oi];
   }
+  c.bpc = bpc;
   const uint32_t units = rtw_total_units(p);
   const uint32_t want = (units + 255) / 256;
   c.grid = std::max(1u, std::min((uint32_t)(rtw_device_cus(dev) * bpc), want));
@@ -767,6 +790,24 @@ size_t rtw_world_workspace_bytes(rtw_world w, const rtw_params* p) {
   }
   const WorldLaunchCfg c = world_cfg(w, p, dev);
   return c.ring_off + c.ring_bytes;
+}
+
+int rtw_world_launch_info(rtw_world w, const rtw_params* p, uint32_t info_out[6]) {
+  if (!w || !info_out) return rtw_fail(RTW_EINVAL, "world/info is NULL");
+  const int v = rtw_validate_params(p);
+  if (v != RTW_OK) return v;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev != w->device)
+    return rtw_fail(RTW_EINVAL, "rtw_world_launch_info: the world's device must be current");
+  const WorldLaunchCfg c = world_cfg(w, p, dev);
+  info_out[0] = w->view.n_nodes == 0 ? RTW_WORLD_TRAVERSAL_LINEAR
+                                     : ((c.fs & 16) ? RTW_WORLD_TRAVERSAL_LANE : RTW_WORLD_TRAVERSAL_UNION);
+  info_out[1] = (uint32_t)c.fs;
+  info_out[2] = (uint32_t)c.oi;
+  info_out[3] = (uint32_t)c.bpc;
+  info_out[4] = c.grid;
+  info_out[5] = (uint32_t)c.lds;
+  return RTW_OK;
 }
 
 int rtw_world_render_device(rtw_world w, const rtw_camera* cam, const rtw_params* p, void* ws, size_t ws_bytes,

@@ -94,6 +94,8 @@ def _wlib():
                                           C.c_uint64 * 4]
     L.rtw_world_render_counts_ex.argtypes = [C.c_void_p, P(Camera), P(Params), C.c_void_p, C.c_size_t,
                                              C.c_uint64 * 8]
+    if hasattr(L, "rtw_world_launch_info"):  # (A/B timing may load an older build without it)
+        L.rtw_world_launch_info.argtypes = [C.c_void_p, P(Params), C.c_uint32 * 6]
     L._world_ready = True
     return L
 
@@ -270,6 +272,9 @@ def render_world(cam: Camera, desc: WorldDesc, params: Params, want_mean=False):
     return (rgb, mean) if want_mean else rgb
 
 
+TRAVERSAL_NAMES = {1: "union", 2: "lane", 3: "linear"}  # rtw_world_traversal (rtw_hip.h)
+
+
 class DeviceWorld:
     """A world resident in HBM of the current device (rtw_world_create)."""
 
@@ -299,15 +304,27 @@ class DeviceWorld:
                                                C.c_void_p(stream) if stream else None,
                                                timer.h if timer is not None else None))
 
+    def launch_info(self, params: Params) -> dict:
+        """rtw_world_launch_info: how a render with these params launches on the
+        current device — the traversal that runs (after AUTO and the world's
+        limits), kernel feature set, register budget, workgroups per CU, grid, LDS."""
+        out = (C.c_uint32 * 6)()
+        _check(_wlib().rtw_world_launch_info(self.h, C.byref(params), out))
+        return {"traversal": TRAVERSAL_NAMES.get(int(out[0]), str(out[0])), "feature_set": int(out[1]),
+                "waves": int(out[2]), "blocks_per_cu": int(out[3]), "grid": int(out[4]), "lds_bytes": int(out[5])}
+
     def counts(self, cam: Camera, params: Params, workspace_ptr: int, workspace_bytes_: int) -> dict:
         """rtw_world_render_counts_ex: the counts, the persistent kernel's wave
-        iterations and whether tail dealing ran (the workspace held the rings)."""
+        iterations and whether tail dealing ran (the workspace held the rings),
+        plus the traversal that ran (rtw_world_launch_info)."""
         out = (C.c_uint64 * 8)()
         _check(_wlib().rtw_world_render_counts_ex(self.h, C.byref(cam), C.byref(params),
                                                   C.c_void_p(workspace_ptr), workspace_bytes_, out))
         return {"samples": int(out[0]), "segments": int(out[1]), "node_visits": int(out[2]),
                 "prim_tests": int(out[3]), "wave_iters": int(out[4]), "tail_dealing": bool(out[5]),
-                "lane_interior_iters": int(out[6]), "lane_leaf_iters": int(out[7])}
+                "lane_interior_iters": int(out[6]), "lane_leaf_iters": int(out[7]),
+                "traversal": self.launch_info(params)["traversal"] if hasattr(_wlib(), "rtw_world_launch_info")
+                else None}
 
     def close(self):
         if self.h:

@@ -138,3 +138,30 @@ def test_design_has_no_unfilled_template_tokens():
             continue
         bad.append(tok)
     assert not bad, sorted(bad)
+
+
+def test_wavefront_rooflines_count_the_bounces_per_launch():
+    """with --engine wavefront --wf-bounces K the headline roofline
+    counted the queue bytes of K = 1 (K times too many).  Both wavefront
+    rooflines take their bytes from bench.wf_frame_bytes: the fused form
+    crosses the queues once per K segments, the split form once per segment."""
+    import importlib
+    import sys
+    from types import SimpleNamespace
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module("bench")
+    counts = {"segments": 1_000_000, "samples": 400_000, "drain_segments": 50_000}
+    units = 30_000
+    for k in (0, 1, 3):
+        a = SimpleNamespace(wf_form="fused", wf_bounces=k, precision="f64")
+        assert bench.wf_frame_bytes(a, counts, units) == bench.wavefront_bytes(counts, "f64", units, True, max(k, 1))
+    a3 = SimpleNamespace(wf_form="fused", wf_bounces=3, precision="f64")
+    a1 = SimpleNamespace(wf_form="fused", wf_bounces=1, precision="f64")
+    fixed = counts["samples"] * (2 * (24 + 4) + 4) + units * 24
+    q1, q3 = bench.wf_frame_bytes(a1, counts, units) - fixed, bench.wf_frame_bytes(a3, counts, units) - fixed
+    assert q1 == 950_000 * 216 and q3 == 950_000 * 216 // 3  # 216 B per queued f64 segment (DESIGN.md §6.2)
+    sp = SimpleNamespace(wf_form="split", wf_bounces=3, precision="f64")
+    assert bench.wf_frame_bytes(sp, counts, units) == bench.wavefront_bytes(counts, "f64", units, False, 1)
+    # the headline path and the variant line both call it
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert src.count("= wf_frame_bytes(args, ") == 2 and "wavefront_bytes(rend.counts" not in src

@@ -189,7 +189,7 @@ def test_product_library_reads_no_environment():
 
 
 @pytest.mark.parametrize("field,value", [("wf_sets", 5), ("wf_drain", 3), ("wf_form", 2), ("world_waves", 5),
-                                         ("world_features", 2), ("world_traversal", 3), ("wf_bounces", 17),
+                                         ("world_waves", 2), ("world_features", 2), ("world_traversal", 3), ("wf_bounces", 17),
                                          ("wf_passes", 65)])
 def test_params_v4_fields_validated(rtw, field, value):
     p = rtw.make_params(64, 36, 1, engine="wavefront")

@@ -330,7 +330,39 @@ def test_globe_bvh_isolates_the_ground_at_the_root():
     assert "node" in lines[1] and "y [0, 4]" in lines[1]
     # the per-lane walk's refs packed into the lower bounds (rtw_world_capi.hip pack_refs): the
     # device's byte gather restated on the host recovers every ref, and no bound moved up
+    # the globe's SAH tree fits the per-lane walk's stack as built (no depth-capped rebuild)
+    dl = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh]") and "depth" in l]
+    assert len(dl) == 1 and re.search(r"depth (\d+) \(unconstrained SAH: \1\)", dl[0]), dl
     packed = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh] packed refs:")]
     assert len(packed) == 1, p.stderr
     m = re.match(r"\[rtw bvh\] packed refs: (\d+) nodes, (\d+) mismatches, bounds moved down by <= (\d+) ulps", packed[0])
     assert m and int(m.group(1)) > 5000 and int(m.group(2)) == 0 and int(m.group(3)) < 512, packed[0]
+
+
+def test_deep_sphere_world_bvh_capped_for_the_lane_walk():
+    """the per-lane walk keeps its stack in 16 LDS entries per
+    lane.  A >= 10k-sphere world whose binned-SAH tree is deeper than that
+    (helpers.deep_cluster_world: depth 24) is rebuilt by rtw_world_create with
+    SAH splits only while a median subtree still fits (rtw_world_capi.hip
+    Builder depth_cap): depth <= 16, leaves of one, refs packed — the lane walk
+    stays available (the GPU test renders it against the linear loop).  The
+    globe's own SAH tree (depth 16) is kept as built (the globe test above)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "from rtw_amd import world as W\n"
+            "from helpers import deep_cluster_world\n"
+            "from test_gpu_world import _to_desc\n"
+            "prims, mats, tex = deep_cluster_world(W)\n"
+            "d, keep = _to_desc(W, prims, [], tex, mats, [], [])\n"
+            "try:\n    W.DeviceWorld(d, debug_bvh=True).close()\nexcept Exception:\n    pass\n") % (
+        os.path.join(REPO, "raytracinginoneweekend.zig_amd"), os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    line = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh]") and "depth" in l]
+    assert len(line) == 1, p.stderr
+    m = re.match(r"\[rtw bvh\] (\d+) nodes, depth (\d+) \(unconstrained SAH: (\d+)\), max leaf (\d+)", line[0])
+    assert m, line[0]
+    nodes, depth, free_depth, leaf = (int(m.group(i)) for i in range(1, 5))
+    assert nodes >= 10000 and free_depth > 16 and depth <= 16 and leaf == 1, line[0]
+    packed = [l for l in p.stderr.splitlines() if l.startswith("[rtw bvh] packed refs:")]
+    assert len(packed) == 1 and " 0 mismatches" in packed[0], p.stderr

@@ -1,6 +1,7 @@
 """One render of BASELINE configs[1] per precision, for rocprofv3 (kernel
-trace / PMC passes).  Usage: python tools/prof_run.py [f64|f32|both|wf64] [reps]
-(wf64: the same frame on the wavefront engine, BASELINE configs[3])"""
+trace / PMC passes).  Usage: python tools/prof_run.py [f64|f32|both|wf64] [reps] [field=value ...]
+(wf64: the same frame on the wavefront engine, BASELINE configs[3]; field=value: rtw_params
+fields of that render, e.g. wf_sets=1 — the library reads no environment for them)"""
 import os
 import sys
 
@@ -16,6 +17,7 @@ from rtw_amd.device import TorchRenderer  # noqa: E402
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "both"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    kw = {k: int(v) if v.isdigit() else v for k, v in (a.split("=", 1) for a in sys.argv[3:])}
     W, spp = 1200, 500
     H = R.image_height(W, 16 / 9)
     sph, mats, _ = R.cover_scene(42)
@@ -23,9 +25,9 @@ def main():
     rend = TorchRenderer(sph, mats, 0)
     for prec in (["f64", "f32"] if which == "both" else [which]):
         if prec == "wf64":
-            p = R.make_params(W, H, spp, precision="f64", engine="wavefront")
+            p = R.make_params(W, H, spp, precision="f64", engine="wavefront", **kw)
         else:
-            p = R.make_params(W, H, spp, precision=prec)
+            p = R.make_params(W, H, spp, precision=prec, **kw)
         for _ in range(reps):
             rend.render(cam, p)
         torch.cuda.synchronize()
