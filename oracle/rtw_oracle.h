@@ -14,8 +14,9 @@
  *             rayColor.  (main.zig:295-402, hittable.zig, material.zig,
  *             texture.zig, rand.zig, vec.zig, ray.zig.)
  *   Tier B  — the GPU path's contract: identical per-sample semantics, but the
- *             RNG is counter-based: Zig's SplitMix64 with its Weyl counter
- *             split into disjoint 2^16-draw blocks per (seed, pixel, sample),
+ *             RNG is counter-based: SplitMix64's Weyl counter split into
+ *             disjoint 2^16-draw blocks per (seed, pixel, sample), each draw's
+ *             state mixed by four Feistel half-rounds (ro_tb_mix, round 5),
  *             so every sample is independent and random-access; the bounce
  *             recursion is evaluated forward (throughput product); samples are
  *             summed per chunk, chunks summed in order.  Precision f64

@@ -4,9 +4,11 @@
  * TB_REAL = float (precision 1, "f32-hybrid").  TEST INFRASTRUCTURE ONLY.
  *
  * This file IS the written contract the HIP kernel implements:
- *  - per sample: the counter-based SplitMix64 block of (seed, pixel, s)
- *    (rtw_oracle.c tierb_state), pixel = image_row * W + column (image rows
- *    top-first), u64 -> real by Zig's Random.float;
+ *  - per sample: the counter-based block of (seed, pixel, s) on SplitMix64's
+ *    Weyl sequence (rtw_oracle.c tierb_state), each draw mixed by four Feistel
+ *    half-rounds (ro_tb_mix; round 5, SplitMix64's output function before),
+ *    pixel = image_row * W + column (image rows top-first), u64 -> real by
+ *    Zig's Random.float;
  *  - draw order per sample (main.zig:390-392, main.zig:91-100): u jitter,
  *    v jitter, unit-disk rejection pairs, time; then per bounce the material's
  *    draws (rand.zig:22-40, material.zig:44-85);

@@ -356,6 +356,82 @@ __device__ __forceinline__ f2 cull_pair(const PairRec& R_, f2 ox, f2 oy, f2 oz, 
   return pfma(na, cc, pfma(hb, hb, k));
 }
 
+// The same bound with the lane's broadcast operands held two to a 64-bit
+// register pair: {ox, oy}, {oz, dx}, {dy, dz}, {na, k} (8 VGPRs instead of 16
+// for bc() pairs, which hold one value twice).  Each VOP3P operand names the
+// 32-bit half it broadcasts by op_sel / op_sel_hi (lo: 0 / 0, hi: 1 / 1).  The
+// same operations in the same order as cull_pair, so the same bits; inline
+// asm because the compiler materialises a broadcast as a register pair.
+// KP: the pair holding k (its half KH: 0 lo, 1 hi).
+struct CullPairs {
+  f2 oxy, ozdx, dyz, nk;
+};
+__device__ __forceinline__ CullPairs cull_pairs(float ox, float oy, float oz, float dx, float dy, float dz, float na,
+                                                float k) {
+  return {f2{ox, oy}, f2{oz, dx}, f2{dy, dz}, f2{na, k}};
+}
+// {a[H], a[H]} - p (p: an SGPR pair of the record)
+template <int H>
+__device__ __forceinline__ f2 pk_bsub(f2 a, f2 p) {
+  f2 r;
+  if constexpr (H == 0)
+    asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "s"(p));
+  else
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "s"(p));
+  return r;
+}
+// x * {b[1], b[1]}
+__device__ __forceinline__ f2 pk_mul_bhi(f2 x, f2 b) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(x), "v"(b));
+  return r;
+}
+// x * {b[H], b[H]} + c
+template <int H>
+__device__ __forceinline__ f2 pk_fma_b1(f2 x, f2 b, f2 c) {
+  f2 r;
+  if constexpr (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(x), "v"(b), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(x), "v"(b), "v"(c));
+  return r;
+}
+// x * x + {c[H], c[H]}
+template <int H>
+__device__ __forceinline__ f2 pk_sq_b2(f2 x, f2 c) {
+  f2 r;
+  if constexpr (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %1, %2 op_sel_hi:[1,1,0]" : "=v"(r) : "v"(x), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %1, %2 op_sel:[0,0,1] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(x), "v"(c));
+  return r;
+}
+// {a[0], a[0]} * x + c
+__device__ __forceinline__ f2 pk_fma_b0lo(f2 a, f2 x, f2 c) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(x), "v"(c));
+  return r;
+}
+// o - c of both spheres of a record (computed before the callers branch on the
+// record's kind: as asm, the compiler would not share it between the branches)
+struct CullOc {
+  f2 x, y, z;
+};
+__device__ __forceinline__ CullOc cull_oc(const PairRec& R_, const CullPairs& C) {
+  return {pk_bsub<0>(C.oxy, R_.v[0]), pk_bsub<1>(C.oxy, R_.v[1]), pk_bsub<0>(C.ozdx, R_.v[2])};
+}
+template <int MOVING, int KH = 1>
+__device__ __forceinline__ f2 cull_pair_sel(const PairRec& R_, const CullOc& oc, const CullPairs& C, f2 kp, f2 frac) {
+  const f2* P = R_.v;
+  f2 ocx = oc.x, ocy = oc.y, ocz = oc.z;
+  if constexpr (MOVING == 1) ocx = pfma(P[3], frac, ocx);
+  if constexpr (MOVING != 0) ocy = pfma(P[4], frac, ocy);
+  if constexpr (MOVING == 1) ocz = pfma(P[5], frac, ocz);
+  const f2 hb = pk_fma_b1<1>(ocz, C.dyz, pk_fma_b1<0>(ocy, C.dyz, pk_mul_bhi(ocx, C.ozdx)));
+  const f2 cc = pfma(ocz, ocz, pfma(ocy, ocy, pfma(ocx, ocx, P[6])));
+  return pk_fma_b0lo(C.nk, cc, pk_sq_b2<KH>(hb, kp));
+}
+
 template <typename R>
 struct Rec {  // one sphere record of the closest-hit loop
   uint32_t meta;
@@ -926,10 +1002,21 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
     // exact test only on the spheres it could not rule out.
     const float af = (float)a;
     const rtwc::LaneCull lc = rtwc::lane_cull((float)L.o.x, (float)L.o.y, (float)L.o.z, af, S.cull_cmax);
+    const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, S.cull_rho);
+#ifndef RTW_CULL_BC  // (the bc() pair form: -DRTW_CULL_BC, measurement builds)
+    const CullPairs cp = cull_pairs((float)L.o.x, (float)L.o.y, (float)L.o.z, (float)L.d.x, (float)L.d.y, (float)L.d.z,
+                                    lk.na, lk.k);
+#define RTW_CULL_OC(rec) const CullOc oc_ = cull_oc(rec, cp)
+#define RTW_CULL(M, rec, fr) cull_pair_sel<M>(rec, oc_, cp, cp.nk, fr)
+#define RTW_CULL_K(M, rec, kp, fr) cull_pair_sel<M, 0>(rec, cull_oc(rec, cp), cp, kp, fr)
+#else
     const f2 ox = bc((float)L.o.x), oy = bc((float)L.o.y), oz = bc((float)L.o.z);
     const f2 dx = bc((float)L.d.x), dy = bc((float)L.d.y), dz = bc((float)L.d.z);
-    const rtwc::LaneConst lk = rtwc::lane_const(af, lc.alpha, S.cull_rho);
     const f2 na = bc(lk.na), alpha = bc(lk.k);
+#define RTW_CULL_OC(rec) (void)0
+#define RTW_CULL(M, rec, fr) cull_pair<M>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr)
+#define RTW_CULL_K(M, rec, kp, fr) cull_pair<M>(rec, ox, oy, oz, dx, dy, dz, na, kp, fr)
+#endif
     const RTW_CONST f2* ct = reinterpret_cast<const RTW_CONST f2*>(cptr(S.cull));
     const RTW_CONST uint32_t* ctg = cptr(S.cull_tg);
     const RTW_CONST float* ctf = cptr(S.tg_f);
@@ -939,7 +1026,7 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
     R fr_v = (R)0;
     // The pretest of one 64-sphere block: bit 31-r of sk[h] set = sphere
     // base+32h+r proven to miss.
-    auto pretest_block = [&](uint32_t base, f2 ox, f2 oy, f2 oz, f2 dx, f2 dy, f2 dz, uint32_t (&sk)[2]) {
+    auto pretest_block = [&](uint32_t base, uint32_t (&sk)[2]) {
       sk[0] = sk[1] = 0u;
       uint32_t tgp_cur = ~0u;
       f2 fr2 = bc(0.0f);
@@ -955,8 +1042,9 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
             const uint32_t tgp = tgp_nxt;
             tgp_nxt = ctg[p + 1];
             f2 x;
+            RTW_CULL_OC(cur);
             if (p < np_static) {
-              x = cull_pair<0>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+              x = RTW_CULL(0, cur, fr2);
             } else {
               if ((tgp & 0xFFFFu) != tgp_cur) {  // wave-uniform
                 tgp_cur = tgp & 0xFFFFu;
@@ -964,9 +1052,9 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
                 fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
               }
               if ((VAR & kVarYOnly) != 0 && (tgp >> 16) != 0u)
-                x = cull_pair<2>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                x = RTW_CULL(2, cur, fr2);
               else
-                x = cull_pair<1>(cur, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                x = RTW_CULL(1, cur, fr2);
             }
             sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.x), 31);
             sk[h] = __builtin_amdgcn_alignbit(sk[h], __float_as_uint(x.y), 31);
@@ -1031,7 +1119,7 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
           // cluster pretest (bounding spheres as static pair records): bit c = proven miss
           uint32_t cmiss = 0u;
           for (uint32_t q = 0; 2u * q < nb; ++q) {
-            const f2 x = cull_pair<0>(ld_pair(ccl, (cb >> 1) + q), ox, oy, oz, dx, dy, dz, na, kcl, bc(0.0f));
+            const f2 x = RTW_CULL_K(0, ld_pair(ccl, (cb >> 1) + q), kcl, bc(0.0f));
             cmiss |= ((__float_as_uint(x.x) >> 31) << (2u * q)) | ((__float_as_uint(x.y) >> 31) << (2u * q + 1u));
           }
           if (!lc.ok) cmiss = 0u;
@@ -1058,16 +1146,16 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
                 const PairRec rec = ld_pair(cct, p);
                 const uint32_t tgp = cctg[p];
                 f2 x;
+                RTW_CULL_OC(rec);
                 if (tgp & (1u << 17)) {
-                  x = cull_pair<0>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                  x = RTW_CULL(0, rec, fr2);
                 } else {
                   if ((tgp & 0xFFFFu) != tgp_cur) {  // wave-uniform
                     tgp_cur = tgp & 0xFFFFu;
                     const uint32_t g0 = tgp & 0xFFu, g1 = (tgp >> 8) & 0xFFu;
                     fr2 = f2{(tf - ctf[4 * g0]) * ctf[4 * g0 + 2], (tf - ctf[4 * g1]) * ctf[4 * g1 + 2]};
                   }
-                  x = (tgp & (1u << 16)) ? cull_pair<2>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2)
-                                         : cull_pair<1>(rec, ox, oy, oz, dx, dy, dz, na, alpha, fr2);
+                  x = (tgp & (1u << 16)) ? RTW_CULL(2, rec, fr2) : RTW_CULL(1, rec, fr2);
                 }
                 b8 = __builtin_amdgcn_alignbit(b8, __float_as_uint(x.x), 31);
                 b8 = __builtin_amdgcn_alignbit(b8, __float_as_uint(x.y), 31);
@@ -1102,12 +1190,12 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
     if (!clustered_done)
     for (uint32_t base = 0; base < S.nn; base += 64) {
       uint32_t sk[2];
-      pretest_block(base, ox, oy, oz, dx, dy, dz, sk);
-      if constexpr ((VAR & 2048) != 0) {  // measurement: the block twice (same image)
-        f2 ox2 = ox, dx2 = dx;
-        asm volatile("" : "+v"(ox2), "+v"(dx2));
+      pretest_block(base, sk);
+      if constexpr ((VAR & 2048) != 0) {  // measurement: the block twice (same image; round 1's phase costs)
+        uint32_t base2 = base;
+        asm volatile("" : "+s"(base2));
         uint32_t sk2[2];
-        pretest_block(base, ox2, oy, oz, dx2, dy, dz, sk2);
+        pretest_block(base2, sk2);
         asm volatile("" ::"v"(sk2[0]), "v"(sk2[1]));
       }
       const uint32_t rem = S.nn - base;  // real spheres in this block

@@ -184,7 +184,11 @@ __device__ __forceinline__ void wave_own_writes_visible() {
 
 // Waves are persistent over segments: wave w owns segments w, w + nwaves, ...
 // for the whole frame (the host launches the same grid every time).
-__device__ __forceinline__ uint32_t wave_id() { return blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6); }
+// (wave-uniform by construction, made so for the compiler: as a per-lane value the
+// segment loop's index lived in a VGPR pair that wf_step spilled to scratch)
+__device__ __forceinline__ uint32_t wave_id() {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6)));
+}
 __device__ __forceinline__ uint32_t wave_count() { return gridDim.x * (kTraceBlock / 64); }
 
 // Workgroup-uniform: does any segment of this workgroup's waves hold paths?
