@@ -80,12 +80,12 @@ def parse():
     return parse_args()
 
 
-EVIDENCE_ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # newest first
+EVIDENCE_ROUNDS = ("r06", "r05", "r04", "r03", "r02", "r01")  # newest first
 
 
 def evidence(name):
     """Path of a committed PMC evidence file: the newest round's copy
-    (profiles/r04, else r03, r02, r01)."""
+    (profiles/r06, else r05, r04, ...)."""
     for rnd in EVIDENCE_ROUNDS:
         path = os.path.join(REPO, "profiles", rnd, name)
         if os.path.exists(path):
@@ -295,13 +295,27 @@ def world_roofline(scene, s, kernel_ms, info, lane=False):
     insts = t["counters"]["SQ_INSTS_VALU"]
     achieved = insts / (kernel_ms * 1e-3) / 1e9
     peak = 1024 * t["clock_ghz"] / 4
-    return {"bound": bound, "achieved": round(achieved, 1), "peak": round(peak, 1),
-            "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4),
-            "traffic": round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"]),
-            "valu_busy_frac_pmc": t["valu_busy_frac"], "wait_frac_of_wave_cycles": t["wait_frac_of_wave_cycles"],
-            "valu_per_wave_iteration": t["valu_per_wave_iteration"], "kernel": "world_kernel",
-            **({"td_busy_frac_pmc": t["td_busy_frac"], "ta_busy_frac_pmc": t["ta_busy_frac"]} if "td_busy_frac" in t else {}),
-            "source": os.path.relpath(path, REPO)}
+    valu = {"achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G wave64 VALU instructions/s",
+            "frac": round(achieved / peak, 4)}
+    common = {"traffic": round(t["hbm_fetch_bytes"] + t["hbm_write_bytes"]),
+              "valu_busy_frac_pmc": t["valu_busy_frac"], "wait_frac_of_wave_cycles": t["wait_frac_of_wave_cycles"],
+              "valu_per_wave_iteration": t["valu_per_wave_iteration"], "kernel": "world_kernel",
+              "source": os.path.relpath(path, REPO)}
+    if lane and "td_busy_frac" in t:
+        # The per-lane walk is bound by the vector memory pipeline's per-lane
+        # data return: every node visit is three 16-B per-lane
+        # loads and every primitive test seven, returned through the CU's TD.
+        # achieved = the TD-busy cycles of the PMC launch (TD_TD_BUSY summed
+        # over the 256 TDs) / the launch time measured here; peak = every TD
+        # busy every cycle (256 x clock).  VALU issue rides along as a side field.
+        tdc = t["vmem_counters"]["TD_TD_BUSY_sum"]
+        a_td = tdc / (kernel_ms * 1e-3) / 1e9
+        p_td = 256 * t["clock_ghz"]
+        return {"bound": "vmem-return (TD: " + trav + ")", "achieved": round(a_td, 1), "peak": round(p_td, 1),
+                "unit": "G TD-busy cycles/s", "frac": round(a_td / p_td, 4), "valu_issue": valu,
+                "td_busy_frac_pmc": t["td_busy_frac"], "ta_busy_frac_pmc": t["ta_busy_frac"], **common}
+    return {"bound": bound, **valu, **common,
+            **({"td_busy_frac_pmc": t["td_busy_frac"], "ta_busy_frac_pmc": t["ta_busy_frac"]} if "td_busy_frac" in t else {})}
 
 
 class ClockWindow:
@@ -366,6 +380,7 @@ def world_variant(R, torch, scene, steps, warmup):
         t.close()
     c = dw.counts(cam, p, ptr, need)
     info = dw.bvh_info()
+    launch = dw.launch_info(p)
     dw.close()
     samples = s.width * s.height * s.spp
     lane = c.get("lane_interior_iters", 0) > 0
@@ -376,7 +391,7 @@ def world_variant(R, torch, scene, steps, warmup):
             "traversal": ("per-lane walks" if lane else "wave union") if info["nodes"] else "linear",
             "config": {"scene": scene, "name": Wd.SCENES[scene], "width": s.width,
                                                   "height": s.height, "spp": s.spp, "max_depth": DEPTH},
-            "bvh": info, "segments_per_sample": round(c["segments"] / samples, 3),
+            "bvh": info, "launch": launch, "segments_per_sample": round(c["segments"] / samples, 3),
             "node_visits_per_segment": round(c["node_visits"] / max(1, c["segments"]), 2),
             "prim_tests_per_segment": round(c["prim_tests"] / max(1, c["segments"]), 2),
             "roofline": roof,

@@ -7,7 +7,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp RTW_WF_TIMEOUT_S=60
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 mkdir -p gpurun_out/ev profiles/$TAG
 ev() { cp "$1" profiles/$TAG/ && cp "$1" gpurun_out/ev/; }
 bash tools/gpu_tests.sh &&
