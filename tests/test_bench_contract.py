@@ -11,7 +11,7 @@ import os
 
 from conftest import REPO
 
-ROUND = "r05"
+ROUND = "r06"
 BENCH = os.path.join(REPO, "profiles", ROUND, "bench.json")
 
 
@@ -142,7 +142,7 @@ def test_design_has_no_unfilled_template_tokens():
     known = set(re.findall(r"\b[A-Z][A-Z0-9]*(?:_[A-Z0-9]+)+\b", open(os.path.join(REPO, "include", "rtw_hip.h")).read()))
     bad = []
     for tok in set(re.findall(r"\b[A-Z][A-Z0-9]*(?:_[A-Z0-9]+)+\b", txt)):
-        if tok.startswith(("RTW_", "DRTW_", "DBL_", "FLT_", "SQ_", "TCC_", "TCP_", "GRBM_", "HSA_", "GPU_", "HIP_",
+        if tok.startswith(("RTW_", "DRTW_", "DBL_", "FLT_", "SQ_", "TCC_", "TCP_", "TD_", "TA_", "GRBM_", "HSA_", "GPU_", "HIP_",
                            "OMP_", "MAX_")) or tok in known:
             continue
         if tok in ("FETCH_SIZE", "WRITE_SIZE", "VAR_BIT", "TIER_A", "TIER_B") or tok.endswith(("_MHZ", "_MS")):
@@ -176,3 +176,23 @@ def test_wavefront_rooflines_count_the_bounces_per_launch():
     # the headline path and the variant line both call it
     src = open(os.path.join(REPO, "bench.py")).read()
     assert src.count("= wf_frame_bytes(args, ") == 2 and "wavefront_bytes(rend.counts" not in src
+
+
+def test_design_pmc_shares_are_the_committed_json():
+    """the pipe shares and write bytes DESIGN.md §0 quotes for the
+    world kernel (VALU busy, TD busy, TA busy, WRITE_SIZE per launch) are the
+    committed PMC JSON's, rounded as printed."""
+    import re
+    text = open(os.path.join(REPO, "DESIGN.md")).read()
+    rows = re.findall(r"^\| [^|`]*\(`profiles/(r\d\d)/(world_pmc_\d\.json)`\) \| ([\d.]+) \| ([\d.]+) \| ([\d.]+) \| "
+                      r"([\d.]+) GB \|", text, re.M)
+    assert len(rows) == 2, rows
+    for rnd, name, valu, td, ta, wr in rows:
+        assert rnd == ROUND, (rnd, name)
+        t = load(name, rnd)
+        for quoted, val in ((valu, t["valu_busy_frac"]), (td, t["td_busy_frac"]), (ta, t["ta_busy_frac"]),
+                            (wr, t["hbm_write_bytes"] / 1e9)):
+            digits = len(quoted.split(".")[1])
+            assert abs(float(quoted) - val) <= 0.5 * 10 ** -digits + 1e-12, (name, quoted, val)
+    # the globe's write-back of round 5's in-loop spill is gone (VERDICT r5 ask 1: <= 0.2 GB per launch)
+    assert load("world_pmc_7.json")["hbm_write_bytes"] <= 0.2e9
