@@ -401,7 +401,9 @@ def world_variant(R, torch, scene, steps, warmup):
 def wavefront_bytes(counts, precision, units, fused=True, bounces=1):
     """Algorithmic HBM bytes of one wavefront frame (rtw_wavefront.hip): per
     bounce segment of the fused engine (default), wf_step reads the path +
-    its hit (root, winner) and writes the next path + its hit; of the split
+    its hit winner and writes the next path + its winner (since round 6 a hit
+    path's origin IS its hit point, so the root is not stored: 200 B f64,
+    216 B before); of the split
     engine (--wf-form split), extend reads o, d, time (+ the skip word in f32)
     and writes (root, winner), shade reads the path + (root, winner) and
     writes the path.  Per sample: the home slot's unit, sample index and f64x3 sum
@@ -413,8 +415,8 @@ def wavefront_bytes(counts, precision, units, fused=True, bounces=1):
     the queues once per `bounces` segments."""
     r = 8 if precision == "f64" else 4
     path = 10 * r + 8 + 4 + 4
-    if fused:  # fused engine: path + hit read, path + hit written
-        seg = 2 * (path + r + 4)
+    if fused:  # fused engine: path + hit winner read, path + winner written (o = the hit point: no root)
+        seg = 2 * (path + 4)
     else:  # extend reads o, d, time (+ skip), writes the hit; shade reads path + hit, writes the path
         seg = (7 * r + (4 if precision == "f32" else 0)) + (r + 4) + (path + r + 4) + path
     queued = counts["segments"] - counts.get("drain_segments", 0)

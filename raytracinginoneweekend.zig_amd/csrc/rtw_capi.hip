@@ -566,7 +566,9 @@ struct WsLayout {
 };
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Byte size of one SoA path queue of n entries (10 R arrays, rs, slot, dsk, + the fused engine's hit root, winner).
-size_t wf_queue_bytes(size_t n, size_t r) { return 11 * al256(n * r) + al256(n * 8) + 3 * al256(n * 4); }
+// (10 R fields, the RNG state, slot, depth|skip, the fused engine's hit winner; round 6 dropped the
+// hit root: a queued hit path carries its hit point in o)
+size_t wf_queue_bytes(size_t n, size_t r) { return 10 * al256(n * r) + al256(n * 8) + 3 * al256(n * 4); }
 WsLayout ws_layout(const rtw_params* p) {
   WsLayout w;
   w.partial_off = 0;
@@ -732,8 +734,6 @@ rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
   b += al256(n * 4);
   q.dsk = reinterpret_cast<uint32_t*>(b);
   b += al256(n * 4);
-  q.ht = reinterpret_cast<R*>(b);
-  b += al256(n * sizeof(R));
   q.hk = reinterpret_cast<int32_t*>(b);
   b += al256(n * 4);
   return q;
@@ -878,6 +878,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     a.batch = refill;
     a.bounces = bounces;
     a.passes = passes;
+    a.hit_form = fused ? 1u : 0u;  // fused: queued paths carry their hit (hk, o = the hit point)
     S.s = k == 0 ? stream : wf_side_stream(dev, k);  // (set 0: the caller's stream, NULL = the default stream)
     if (k > 0 && !S.s) {
       st = fail(RTW_EHIP, "wavefront side stream creation failed");

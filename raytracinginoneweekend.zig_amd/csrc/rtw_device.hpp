@@ -1228,13 +1228,15 @@ __device__ __forceinline__ void closest_hit(const SV& S, const LdsTables<R>& T, 
 // attenuation product and depth move to the next segment.
 // PRE: the dielectric's draw was made by coop_reject_mixed (`draw`, the draw
 // at state L.rs + gamma); it is consumed only when the reference draws it.
-template <typename R, bool F32, int VAR = 0, bool PRE = false>
+// POINT: L.o already holds the hit point p = o + tmax * d (the wavefront's
+// path form, made with these operations where the hit was found), tmax unused.
+template <typename R, bool F32, int VAR = 0, bool PRE = false, bool POINT = false>
 __device__ __forceinline__ bool scatter_hit(const LdsTables<R>& T, Lane<R>& L, int hit, R tmax, uint32_t kind,
                                             const R (&b3)[3], R draw = (R)0) {
   // Hit record of the winner (hittable.zig:118-128, :189-198).
   const R* sp = T.sph + 8 * hit;
   const uint32_t meta = T.meta[hit];
-  const V3<R> p = add(L.o, mul(L.d, tmax));
+  const V3<R> p = POINT ? L.o : add(L.o, mul(L.d, tmax));  // ray.at(t) (ray.zig)
   V3<R> center = ld3(sp);
   if (meta & kMoving) {
     const uint32_t g = (meta >> 2) & 63u;

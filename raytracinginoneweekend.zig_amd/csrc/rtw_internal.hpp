@@ -165,8 +165,8 @@ struct PathBuf {
   uint64_t* rs;
   uint32_t* slot;  // home slot
   uint32_t* dsk;   // depth | (skip + 1) << 16
-  R* ht;           // fused engine: root of the path's closest hit (computed where the ray was made)
-  int32_t* hk;     // fused engine: its table position, -1 = miss
+  int32_t* hk;     // fused engine: the table position of the path's closest hit, -1 = miss; with hk >= 0 the path's
+                   // o holds the hit point o + t * d (made where the hit was found: wavefront.hip to_hit_point)
 };
 // Moving bytes per path (one PathBuf entry).
 template <typename R>
@@ -191,6 +191,8 @@ struct WfArgs {
   uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
   uint32_t bounces;    // wf_step: bounce segments per path per launch (>= 1), the path kept in registers between them
   uint32_t passes;     // wf_step: queue passes per launch (>= 1): in -> out, out -> in, ... (every segment through the queues)
+  uint32_t hit_form;   // 1: queue `in` holds paths WITH their hit (fused engine: hk, and o = the hit point); the drains
+                       // then shade the stored hit first instead of tracing the segment again
 };
 
 hipError_t launch_wf_generate_f64(const WfArgs<double>& a, uint32_t grid, size_t lds, hipStream_t s);

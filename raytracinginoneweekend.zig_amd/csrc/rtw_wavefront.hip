@@ -150,18 +150,29 @@ __device__ __forceinline__ void push_path(const PathBuf<R>& out, uint32_t seg_ba
   out_n += (uint32_t)__popcll(m);
 }
 
-// The same with the path's closest hit (fused engine).
+// The same with the path's closest hit (fused engine): its table position;
+// L.o is already the hit point (to_hit_point), so the root is not stored.
 template <typename R>
 __device__ __forceinline__ void push_path_hit(const PathBuf<R>& out, uint32_t seg_base, uint32_t& out_n, bool live,
-                                              const Lane<R>& L, uint32_t slot, int hit, R tmax) {
+                                              const Lane<R>& L, uint32_t slot, int hit) {
   const uint64_t m = __ballot(live);
   if (live) {
     const uint32_t i = seg_base + out_n + mbcnt64(m);
     store_path(out, i, L, slot);
-    out.ht[i] = tmax;
     out.hk[i] = hit;
   }
   out_n += (uint32_t)__popcll(m);
+}
+
+// Round 6: a path that found its closest hit carries the hit POINT in its
+// origin from then on: p = o + t * d — ray.at(t), the operations scatter_hit
+// makes (rtw_device.hpp, POINT = false), made here instead, so the same bits.
+// The shading reads p (scatter_hit POINT), never o and t; the queues move
+// p (24 B) instead of o and the root (32 B): 200 instead of 216 B per bounce
+// segment of the fused engine.
+template <typename R>
+__device__ __forceinline__ void to_hit_point(Lane<R>& L, int hit, R tmax) {
+  if (hit >= 0) L.o = add(L.o, mul(L.d, tmax));
 }
 
 template <typename R>
@@ -231,7 +242,7 @@ __device__ __forceinline__ void bounce(const WfArgs<R>& A, const LdsTables<R>& T
   R b3[3] = {(R)0, (R)0, (R)0};
   if (__any(nb)) coop_reject<R, 3, true>(nb, L.rs, b3, T.slots, lid);
   if (shading) {
-    if (scatter_hit<R, F32>(T, L, hit, tmax, kind, b3))
+    if (scatter_hit<R, F32, 0, false, true>(T, L, hit, tmax, kind, b3))
       ended = true;  // absorbed: emitted == 0 (material.zig:31-38)
     else if (L.depth == A.t.max_depth)
       ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
@@ -344,8 +355,11 @@ __global__ void __launch_bounds__(kTraceBlock) wf_generate(WfArgs<R> A) {
       if constexpr (HIT) {
         int hit = -1;
         R tmax = (R)__builtin_huge_val();
-        if (got) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, hit, tmax);
-        push_path_hit(A.out, base, out_n, got, L, slot, hit, tmax);
+        if (got) {
+          closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, hit, tmax);
+          to_hit_point(L, hit, tmax);
+        }
+        push_path_hit(A.out, base, out_n, got, L, slot, hit);
       } else {
         push_path(A.out, base, out_n, got, L, slot);
       }
@@ -440,6 +454,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
       load_path(A.in, i, L, slot);
       hit = A.hit_k[i];
       tmax = A.hit_t[i];
+      to_hit_point(L, hit, tmax);
     }
     const bool live = shade_step<R, F32, STATS>(A, T, lid, valid, L, slot, hit, tmax, qnext, qend);
     push_path(A.out, base, out_n, live, L, slot);
@@ -491,14 +506,29 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
   // what lane 0 wrote in the pass before; the scalar cache would not see it).
   auto step_segment = [&](uint32_t seg, const PathBuf<R>& qin, const PathBuf<R>& qout, const uint32_t* sin,
                           uint32_t* sout) {
+    const uint32_t base = seg * kSegCap;
+    const uint32_t i = base + lid;
+#ifndef RTW_WF_LOAD_AFTER_COUNT
+    // The segment's count, reservoir and paths are loaded together: the path
+    // loads of every lane (in bounds: a segment holds kSegCap positions) are
+    // issued before the count is known, so the segment start waits for one
+    // memory latency, not for the count's and then the paths' (a dependent
+    // chain).  Lanes past the count ignore what they loaded.
+    const uint32_t n_in = ld_wave_u32(sin + seg);
+    uint32_t qnext = ld_wave_u32(A.seg_resv + 2 * seg), qend = ld_wave_u32(A.seg_resv + 2 * seg + 1), out_n = 0;
+    int hit = qin.hk[i];
+    R tmax = (R)0;  // (the stored path's o is its hit point)
+    Lane<R> L{};
+    uint32_t slot = 0;
+    load_path(qin, i, L, slot);
+    const bool valid = lid < n_in;  // (an empty segment runs through with no lane valid: out_n = 0)
+#else
     const uint32_t n_in = ld_wave_u32(sin + seg);
     if (n_in == 0u) {
       if (lid == 0) sout[seg] = 0u;
       return;
     }
-    const uint32_t base = seg * kSegCap;
     uint32_t qnext = ld_wave_u32(A.seg_resv + 2 * seg), qend = ld_wave_u32(A.seg_resv + 2 * seg + 1), out_n = 0;
-    const uint32_t i = base + lid;
     const bool valid = lid < n_in;
     Lane<R> L{};
     L.skip = -1;
@@ -508,8 +538,8 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
     if (valid) {
       load_path(qin, i, L, slot);
       hit = qin.hk[i];
-      tmax = qin.ht[i];
     }
+#endif
     // A.bounces (>= 1) bounce segments per path in this launch: shade, then
     // the next ray's closest hit, with the path kept in registers between
     // them (one queue read and one write per A.bounces segments; the same
@@ -521,10 +551,13 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
       live = shade_step<R, F32, STATS>(A, T, lid, live, L, slot, nh, nt, qnext, qend);
       nh = -1;
       nt = (R)__builtin_huge_val();
-      if (live) closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
+      if (live) {
+        closest_hit<R, F32, 0, kWfExtendVar<R>>(opaque(kargs<R>())->sc, T, L, A.t.tmin, A.t.pre_k, lid, st, nh, nt);
+        to_hit_point(L, nh, nt);
+      }
       if (!wany(live)) break;
     }
-    push_path_hit(qout, base, out_n, live, L, slot, nh, nt);
+    push_path_hit(qout, base, out_n, live, L, slot, nh);
     if (lid == 0) {
       sout[seg] = out_n;
       A.seg_resv[2 * seg] = qnext;
@@ -577,11 +610,22 @@ __global__ void __launch_bounds__(kTraceBlock) wf_finish(WfArgs<R> A) {
     L.skip = -1;
     uint32_t slot = 0;
     bool live = lid < n_in;
-    if (live) load_path(A.in, seg * kSegCap + lid, L, slot);
+    int hit0 = -1;
+    if (live) {
+      load_path(A.in, seg * kSegCap + lid, L, slot);
+      if (A.hit_form) hit0 = A.in.hk[seg * kSegCap + lid];
+    }
+    bool stored = A.hit_form != 0u;  // the queued paths carry their hit: shade it first
     while (__any(live)) {  // wave-converged loop; a lane's path advances one segment per pass
       int hit = -1;
       R tmax = (R)__builtin_huge_val();
-      if (live) closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+      if (stored) {
+        hit = hit0;
+      } else if (live) {
+        closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+        to_hit_point(L, hit, tmax);
+      }
+      stored = false;
       live = shade_step<R, F32, STATS, true>(A, T, lid, live, L, slot, hit, tmax, qnext, qend);
     }
     if (lid == 0) {
@@ -649,9 +693,11 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain([[maybe_unused]] WfArgs<
     L.skip = -1;
     uint32_t k = 0;  // the slot whose sample this lane traces
     bool have = lid < n_in;
+    int stored = -2;  // hit_form: the queued path's hit, shaded before the lane traces again (-2: none)
     if (have) {  // the in-flight sample of slot k, from queue A
       uint32_t slot;
       load_path(A.in, base + lid, L, slot);
+      if (A.hit_form) stored = A.in.hk[base + lid];
       k = slot - base;
       const uint32_t unit = A.home[slot].unit, s = A.home[slot].s;
       uint32_t px, ly, c;
@@ -700,7 +746,15 @@ __global__ void __launch_bounds__(kTraceBlock) wf_drain([[maybe_unused]] WfArgs<
       // 2. One segment of every lane's path.
       int hit = -1;
       R tmax = (R)__builtin_huge_val();
-      if (have) closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+      if (have) {
+        if (stored != -2) {  // (its o is the hit point already)
+          hit = stored;
+          stored = -2;
+        } else {
+          closest_hit<R, F32, 0, 0>(S, T, L, tmin, pre_k, lid, st, hit, tmax);
+          to_hit_point(L, hit, tmax);
+        }
+      }
       bool ended, miss;
       bounce<R, F32>(A, T, lid, have, L, hit, tmax, ended, miss);
       if constexpr (STATS) {

@@ -170,7 +170,7 @@ def test_wavefront_rooflines_count_the_bounces_per_launch():
     a1 = SimpleNamespace(wf_form="fused", wf_bounces=1, precision="f64")
     fixed = counts["samples"] * (2 * (24 + 4) + 4) + units * 24
     q1, q3 = bench.wf_frame_bytes(a1, counts, units) - fixed, bench.wf_frame_bytes(a3, counts, units) - fixed
-    assert q1 == 950_000 * 216 and q3 == 950_000 * 216 // 3  # 216 B per queued f64 segment
+    assert q1 == 950_000 * 200 and q3 == 950_000 * 200 // 3  # 200 B per queued f64 segment
     sp = SimpleNamespace(wf_form="split", wf_bounces=3, precision="f64")
     assert bench.wf_frame_bytes(sp, counts, units) == bench.wavefront_bytes(counts, "f64", units, False, 1)
     # the headline path and the variant line both call it

@@ -113,7 +113,8 @@ def test_workspace_bytes(rtw):
 @pytest.mark.parametrize("ring", [True, False])
 def test_workspace_bytes_wavefront(rtw, monkeypatch, sets, ring):
     """Wavefront engine: + two SoA path queues (each with the fused engine's
-    hit root / winner per path), the split engine's hit arrays, the home
+    hit winner per path; its hit point rides in the path's origin since round 6),
+    the split engine's hit arrays, the home
     slots and (wf_drain only: params.wf_drain RTW_WF_DRAIN_SAMPLES) its ring of 32 R x3 sample
     radiances (rtw_capi.hip ws_layout) per in-flight path, + per-segment
     words; wf_paths is split over params.wf_sets queue sets, so the bytes per
@@ -124,7 +125,7 @@ def test_workspace_bytes_wavefront(rtw, monkeypatch, sets, ring):
         for n in (1 << 16, 1 << 20, 3 << 18):
             p = rtw.make_params(1200, 675, 500, precision=prec, engine="wavefront", wf_paths=n, wf_sets=sets,
                                 wf_drain="samples" if ring else "slots")
-            per_path = 2 * (10 * r + 8 + 4 + 4 + r + 4) + (r + 4) + 32 + (32 * 3 * r if ring else 0)
+            per_path = 2 * (10 * r + 8 + 4 + 4 + 4) + (r + 4) + 32 + (32 * 3 * r if ring else 0)
             segs = -(-n // (64 * sets))  # per set: one 64-path queue segment = 2 counts + a unit reservoir
             paths = segs * 64
             extra = rtw.workspace_bytes(p) - base
