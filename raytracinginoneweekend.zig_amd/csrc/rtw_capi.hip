@@ -574,7 +574,7 @@ WsLayout ws_layout(const rtw_params* p) {
   w.partial_off = 0;
   w.partial_bytes = (size_t)n_chunks(p) * p->row_count * p->width * 3 * sizeof(double);
   w.counter_off = al256(w.partial_bytes);
-  w.live_off = w.counter_off + 64;  // kWfMaxSets words
+  w.live_off = w.counter_off + 64;  // kWfMaxSets words; + 128: wf_step's live_acc pairs (kWfMaxSets x 2 words)
   w.stats_off = w.counter_off + 256;
   w.total = w.stats_off + 256;  // stats: 32 x u64
   w.wf_off = w.total;
@@ -741,12 +741,18 @@ rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
 
 // Thread-local pinned words the host polls for the queue lengths (two per
 // queue set: batches are checked one behind).
+// Mapped: the fused engine's wf_step writes its batch's word from the device
+// (poll_words_dev: the device address of the same words).
 uint32_t* poll_words() {
   thread_local uint32_t* w = nullptr;
-  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * kWfMaxSets * sizeof(uint32_t), hipHostMallocPortable) !=
-                hipSuccess)
+  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * kWfMaxSets * sizeof(uint32_t),
+                          hipHostMallocPortable | hipHostMallocMapped) != hipSuccess)
     w = nullptr;
   return w;
+}
+uint32_t* poll_words_dev(uint32_t* host) {
+  void* d = nullptr;
+  return host && hipHostGetDevicePointer(&d, host, 0) == hipSuccess ? static_cast<uint32_t*>(d) : nullptr;
 }
 
 // Side streams of the wavefront queue sets 1.. (set 0 runs on the caller's
@@ -847,6 +853,8 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   const int iters = std::max(2, (kWfIters / (int)passes) & ~1);  // even: the batch ends with the paths in queue A
   uint32_t* poll = poll_words();
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
+  uint32_t* poll_dev = poll_words_dev(poll);
+  if (!poll_dev) return fail(RTW_EHIP, "hipHostGetDevicePointer of the poll words failed");
   WfSet<R> set[kWfMaxSets];
   int st = RTW_OK;
   hipEvent_t fork = nullptr;
@@ -879,6 +887,8 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
     a.bounces = bounces;
     a.passes = passes;
     a.hit_form = fused ? 1u : 0u;  // fused: queued paths carry their hit (hk, o = the hit point)
+    a.live_acc = reinterpret_cast<uint32_t*>(ws + L.counter_off + 128) + 2 * k;  // (zeroed with the queue head)
+    a.poll_out = nullptr;  // (set per batch)
     S.s = k == 0 ? stream : wf_side_stream(dev, k);  // (set 0: the caller's stream, NULL = the default stream)
     if (k > 0 && !S.s) {
       st = fail(RTW_EHIP, "wavefront side stream creation failed");
@@ -921,6 +931,9 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       if (S.done) continue;
       rtwk::WfArgs<R>& a = S.a;
       hipError_t e = hipSuccess;
+      // fused: the batch's wf_step launches publish the live count into this
+      // batch's pinned word themselves (wf_step publish_live); split: wf_count + copy
+      a.poll_out = fused ? poll_dev + 2 * k + (S.batch & 1) : nullptr;
       for (int i = 0; i < iters && e == hipSuccess; ++i) {
         const bool even = (i & 1) == 0 || (passes & 1u) == 0u;  // (an even pass count returns to its input queue)
         a.in = even ? S.qa : S.qb;
@@ -937,10 +950,11 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
         break;
       }
       uint32_t* pw = poll + 2 * k + (S.batch & 1);
-      if (rtwk::launch_wf_count(S.seg_a, segs, a.live, S.s) != hipSuccess ||
-          hipMemcpyAsync(pw, a.live, 4, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+      if ((!fused && (rtwk::launch_wf_count(S.seg_a, segs, a.live, S.s) != hipSuccess ||
+                      hipMemcpyAsync(pw, a.live, 4, hipMemcpyDeviceToHost, S.s) != hipSuccess)) ||
           hipEventRecord(S.ev[S.batch & 1], S.s) != hipSuccess)
         st = fail(RTW_EHIP, "wavefront poll enqueue failed");
+      a.poll_out = nullptr;  // (the drains and checks below do not publish)
     }
     for (uint32_t k = 0; k < nsets && st == RTW_OK; ++k) {
       WfSet<R>& S = set[k];
@@ -1024,7 +1038,8 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
                              : 0u;
   size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
   if (p->engine == RTW_ENGINE_MEGAKERNEL && (var & rtwk::kVarHomeLdsBit) != 0)
-    lds += 8 + rtwk::kHomeLdsBytesPerWave * (rtwk::kTraceBlock / 64);  // (8: alignment of the home block)
+    lds += 8 + (rtwk::kHomeLdsBytesPerWave + ((var & rtwk::kVarPathLdsBit) ? rtwk::kPathLdsBytesPerWave : 0)) *
+                   (rtwk::kTraceBlock / 64);  // (8: alignment of the home block)
   if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);
   const int cus = device_cus(dev);

@@ -83,6 +83,11 @@ constexpr int kVarMergedStart = 262144;
 constexpr int kVarPreDraw = 524288;
 // Unit refill: each 64-unit batch's (tile, chunk) decoded once per batch.
 constexpr int kVarBatchDecode = 1048576;
+// kVarPathLds (with kVarHomeLds and kVarMergedStart): the lane's attenuation T and
+// RNG state live in its LDS home block between the phases that use them
+// (sampler, scatter, sample start, miss), so neither is held in VGPRs across
+// the closest hit.
+constexpr int kVarPathLds = 33554432;
 // f64 pretest over spatial clusters of narrow spheres (SceneView ccull...):
 // a wave skips a cluster's member pretests when every lane's line provably
 // misses the cluster's bounding sphere.

@@ -72,12 +72,23 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   constexpr bool HOME = (VAR & kVarHomeLds) != 0;
   double* h_sum = nullptr;    // [3][64]
   uint32_t* h_u32 = nullptr;  // px[64], ly[64], c[64], s_end[64]
+  R* h_t = nullptr;           // kVarPathLds: T [3][64] (8-B slots)
+  uint64_t* h_rs = nullptr;   // kVarPathLds: RNG state [64]
   if constexpr (HOME) {
     const size_t off = (size_t)(reinterpret_cast<unsigned char*>(T.cpos + kClusterSlots * S.n_clusters) - lds_raw);
-    unsigned char* hb = lds_raw + ((off + 7) & ~(size_t)7) + (threadIdx.x >> 6) * kHomeLdsBytesPerWave;
+    constexpr size_t kHomeStride = kHomeLdsBytesPerWave + ((VAR & kVarPathLds) ? kPathLdsBytesPerWave : 0);
+    unsigned char* hb = lds_raw + ((off + 7) & ~(size_t)7) + (threadIdx.x >> 6) * kHomeStride;
     h_sum = reinterpret_cast<double*>(hb);
     h_u32 = reinterpret_cast<uint32_t*>(hb + 3 * 64 * 8);
+    h_t = reinterpret_cast<R*>(hb + 2560);
+    h_rs = reinterpret_cast<uint64_t*>(hb + 2560 + 3 * 64 * 8);
   }
+  constexpr bool PLDS = HOME && (VAR & kVarPathLds) != 0 && (VAR & kVarMergedStart) != 0;
+  constexpr uint32_t TS = 8 / sizeof(R);  // (8-B slots: T component k of lane l at h_t[(k * 64 + l) * TS])
+  auto t_load = [&]() -> V3<R> { return mk(h_t[lid * TS], h_t[(64 + lid) * TS], h_t[(128 + lid) * TS]); };
+  auto t_store = [&](const V3<R>& v) {
+    h_t[lid * TS] = v.x, h_t[(64 + lid) * TS] = v.y, h_t[(128 + lid) * TS] = v.z;
+  };
   // VAR bit 10: the loop's kernel-argument fields are re-read where used
   // (scalar loads through a laundered kernarg pointer) instead of living in
   // SGPRs for the whole kernel: the SGPR budget is the limit (spills become
@@ -228,7 +239,9 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
     else
       closest_hit<R, F32, MODE, VAR>(S, T, L, tmin, A.pre_k, lid, st, hit, tmax);
     if (hit < 0) {  // miss: background (main.zig:109-112)
-      const V3<R> col = mulv(L.T, ld3(opaque(kargs<R>())->bg));
+      V3<R> tt = L.T;
+      if constexpr (PLDS) tt = t_load();
+      const V3<R> col = mulv(tt, ld3(opaque(kargs<R>())->bg));
       if constexpr (HOME) {
         h_sum[lid] += (double)col.x;
         h_sum[64 + lid] += (double)col.y;
@@ -264,6 +277,7 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       }
       RTW_STAMP(0)
       const bool ns = have_unit && !have_ray;
+      if constexpr (PLDS) L.rs = h_rs[lid];
       R u = (R)0, v = (R)0;
       if (ns) {
         if constexpr (HOME) {
@@ -280,11 +294,16 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, pt, raw, slots, lid);
       RTW_STAMP(7)
       if (shading) {
+        if constexpr (PLDS) L.T = t_load();
         if (scatter_hit<R, F32, VAR, PRE>(T, L, hit, tmax, kind, pt, raw)) finish_sample();  // absorbed
       }
       if (ns) {
         start_sample_ray<R, PRE>(kargs<R>(), L, u, v, pt[0], pt[1], raw);
         have_ray = true;
+      }
+      if constexpr (PLDS) {
+        if (shading || ns) t_store(L.T);
+        h_rs[lid] = L.rs;
       }
       RTW_STAMP(8)
       shading = false;

@@ -488,6 +488,32 @@ template <typename R>
 __device__ __forceinline__ const WfArgs<R>& wkargs() {
   return *(const WfArgs<R>*)opaque((const RTW_CONST WfArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr());
 }
+// The host's poll without a kernel of its own (round 6): every wave of a
+// wf_step launch adds its segments' final path counts (lane 0's `sum`) to
+// live_acc[0]; the launch's last workgroup (a ticket in live_acc[1]) writes
+// the total to the host's pinned poll word and zeroes both words for the next
+// launch.  It replaces, per polled batch, a wf_count launch and the copy of
+// its result, which waited in stream order for a CU the other queue set's
+// wf_step held (~50 us each in the kernel trace).  Release / acquire at agent
+// scope order the adds before the ticket; the kernel's end makes the host
+// word visible to the event the host waits on.
+template <typename R>
+__device__ __forceinline__ void publish_live(const WfArgs<R>& A, uint32_t sum) {
+  if (!A.poll_out) return;  // (wave-uniform: a kernel argument)
+  if ((threadIdx.x & 63u) == 0u && sum) __hip_atomic_fetch_add(A.live_acc, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t t = __hip_atomic_fetch_add(A.live_acc + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1u == gridDim.x) {
+      const uint32_t total = __hip_atomic_load(A.live_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(A.poll_out, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(A.live_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(A.live_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <typename R, bool F32, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_unused]] WfArgs<R> A_arg) {
   extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -496,6 +522,7 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
   if (!group_has_work(A)) {  // every segment of the group is empty: so is its output
     if (lid == 0 && (A.passes & 1u) != 0u)  // (an even pass count ends in seg_in, already all zero)
       for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) A.seg_out[seg] = 0u;
+    publish_live(A, 0u);
     return;
   }
   const LdsTables<R> T = stage_tables<R>(A.t.sc, lds_raw);
@@ -504,8 +531,9 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
   // One queue pass over a segment: qin -> qout.  The segment's count and
   // reservoir are read with vector loads (a later pass of this launch reads
   // what lane 0 wrote in the pass before; the scalar cache would not see it).
+  uint32_t live_sum = 0u;  // (lane 0) the wave's segment counts after the launch's last pass
   auto step_segment = [&](uint32_t seg, const PathBuf<R>& qin, const PathBuf<R>& qout, const uint32_t* sin,
-                          uint32_t* sout) {
+                          uint32_t* sout, bool last) {
     const uint32_t base = seg * kSegCap;
     const uint32_t i = base + lid;
 #ifndef RTW_WF_LOAD_AFTER_COUNT
@@ -562,6 +590,7 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
       sout[seg] = out_n;
       A.seg_resv[2 * seg] = qnext;
       A.seg_resv[2 * seg + 1] = qend;
+      if (last) live_sum += out_n;
     }
   };
   // (Segments dealt at run time instead, one ticket of a device counter per
@@ -578,8 +607,10 @@ __global__ void __launch_bounds__(kTraceBlock, RTW_WF_STEP_OCC) wf_step([[maybe_
     const uint32_t* sin = odd ? A.seg_out : A.seg_in;
     uint32_t* sout = odd ? A.seg_in : A.seg_out;
     if (q > 0) wave_own_writes_visible();
-    for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count()) step_segment(seg, qin, qout, sin, sout);
+    for (uint32_t seg = wave_id(); seg < A.n_segs; seg += wave_count())
+      step_segment(seg, qin, qout, sin, sout, q + 1u == A.passes);
   }
+  publish_live(A, live_sum);
 }
 
 // ------------------------------------------------------------------ finish --

@@ -126,6 +126,19 @@ __device__ __forceinline__ PrimRec load_rec(P r) {
   return q;
 }
 
+// The per-lane walk's record load: doubles 0-10 and the {kind, list index}
+// copy in double 11 (rtw_world_capi.hip), one 96-B span = six 16-B loads.
+template <typename P>
+__device__ __forceinline__ PrimRec load_rec_lane(P r) {
+  PrimRec q;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) q.v[i] = r[i];
+  const uint64_t m = __builtin_bit_cast(uint64_t, (D)r[11]);
+  q.meta0 = (uint32_t)m;
+  q.orig = (uint32_t)(m >> 32);
+  return q;
+}
+
 // A ray in one primitive space with Sphere.hit's `a` = |d|^2 (hittable.zig:97)
 // and ia = RN(1/a): the root divisions run as Markstein div_rn (rtw_math.hpp:
 // RN(x / b) from RN(1 / b), IEEE division outside the normal range), the same
@@ -660,8 +673,8 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
       for (uint32_t k = first; k < first + cnt; ++k) {
         if (MODE == 1) ++nt;
         D t;
-        const PrimRec q = load_rec(reinterpret_cast<GD*>(reinterpret_cast<const __attribute__((address_space(1))) char*>(pr) +
-                                                         (k << 7)));  // (kWorldRec doubles = 128 B)
+        const PrimRec q = load_rec_lane(reinterpret_cast<GD*>(
+            reinterpret_cast<const __attribute__((address_space(1))) char*>(pr) + (k << 7)));  // (kWorldRec doubles = 128 B)
         if (root_obj<true, FEAT>(q, ws, time, tmin, t)) accept(h, t, (int)k, (int)q.orig, tmin);
       }
       tmaxf = round_up(h.t);

@@ -458,6 +458,11 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
     }
     const uint32_t meta[4] = {p.kind | ((uint32_t)(p.xform + 1) << 8), p.mat, li, 0u};
     std::memcpy(r + 14, meta, sizeof(meta));
+    // the kind and list index again in double 11, so the per-lane walk's root
+    // test reads doubles 0-11 only: six 16-B loads per primitive, not seven
+    // (rtw_world.hip load_rec_lane)
+    const uint32_t meta_lane[2] = {meta[0], meta[2]};
+    std::memcpy(r + 11, meta_lane, sizeof(meta_lane));
   }
   // Leaf pretest records (rtw_cull.hpp, the megakernel's packed-f32 bound):
   // a BVH leaf of <= 2 spheres that are untransformed, narrow (|r| < 100) and
