@@ -745,7 +745,7 @@ rtwk::PathBuf<R> carve_queue(unsigned char*& b, size_t n) {
 // (poll_words_dev: the device address of the same words).
 uint32_t* poll_words() {
   thread_local uint32_t* w = nullptr;
-  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * kWfMaxSets * sizeof(uint32_t),
+  if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 4 * kWfMaxSets * sizeof(uint32_t),
                           hipHostMallocPortable | hipHostMallocMapped) != hipSuccess)
     w = nullptr;
   return w;
@@ -855,6 +855,14 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
   if (!poll) return fail(RTW_EHIP, "hipHostMalloc of the poll words failed");
   uint32_t* poll_dev = poll_words_dev(poll);
   if (!poll_dev) return fail(RTW_EHIP, "hipHostGetDevicePointer of the poll words failed");
+  // development knobs: RTW_WF_POLL_KERNEL=1 polls the fused engine through
+  // wf_count + copy as the split form does; RTW_WF_POLL_CHECK=1 runs both and
+  // reports on stderr a batch whose published count differs from wf_count's
+  const char* pk = dev_knob("RTW_WF_POLL_KERNEL");
+  const char* pc = dev_knob("RTW_WF_POLL_CHECK");
+  const bool poll_check = fused && pc && *pc == '1';
+  const bool publish = fused && !(pk && *pk == '1');
+  if (publish && grid_step >= (1u << 20)) return fail(RTW_EINVAL, "wf_step grid %u exceeds the poll ticket's 20 bits", grid_step);
   WfSet<R> set[kWfMaxSets];
   int st = RTW_OK;
   hipEvent_t fork = nullptr;
@@ -933,7 +941,7 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
       hipError_t e = hipSuccess;
       // fused: the batch's wf_step launches publish the live count into this
       // batch's pinned word themselves (wf_step publish_live); split: wf_count + copy
-      a.poll_out = fused ? poll_dev + 2 * k + (S.batch & 1) : nullptr;
+      a.poll_out = publish ? poll_dev + 2 * k + (S.batch & 1) : nullptr;
       for (int i = 0; i < iters && e == hipSuccess; ++i) {
         const bool even = (i & 1) == 0 || (passes & 1u) == 0u;  // (an even pass count returns to its input queue)
         a.in = even ? S.qa : S.qb;
@@ -949,8 +957,8 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
         st = fail(RTW_EHIP, "wavefront bounce launch: %s", hipGetErrorString(e));
         break;
       }
-      uint32_t* pw = poll + 2 * k + (S.batch & 1);
-      if ((!fused && (rtwk::launch_wf_count(S.seg_a, segs, a.live, S.s) != hipSuccess ||
+      uint32_t* pw = poll + (publish ? 2 * kWfMaxSets : 0u) + 2 * k + (S.batch & 1);
+      if (((!publish || poll_check) && (rtwk::launch_wf_count(S.seg_a, segs, a.live, S.s) != hipSuccess ||
                       hipMemcpyAsync(pw, a.live, 4, hipMemcpyDeviceToHost, S.s) != hipSuccess)) ||
           hipEventRecord(S.ev[S.batch & 1], S.s) != hipSuccess)
         st = fail(RTW_EHIP, "wavefront poll enqueue failed");
@@ -966,6 +974,9 @@ int run_wavefront(const rtwk::TraceArgs<R>& ta, const rtw_params* p, unsigned ch
         break;
       }
       const uint32_t live = poll[2 * k + ((b - 1) & 1)];
+      if (poll_check && publish && live != poll[2 * kWfMaxSets + 2 * k + ((b - 1) & 1)])
+        std::fprintf(stderr, "[rtw wf poll] set %u batch %llu: published %u, wf_count %u\n", k,
+                     (unsigned long long)(b - 1), live, poll[2 * kWfMaxSets + 2 * k + ((b - 1) & 1)]);
       if (live != 0u && (double)live < fin_frac * (double)n) {  // queue A holds the paths after this batch
         rtwk::WfArgs<R>& a = S.a;
         a.in = S.qa;
@@ -1038,7 +1049,8 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
                              : 0u;
   size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
   if (p->engine == RTW_ENGINE_MEGAKERNEL && (var & rtwk::kVarHomeLdsBit) != 0)
-    lds += 8 + (rtwk::kHomeLdsBytesPerWave + ((var & rtwk::kVarPathLdsBit) ? rtwk::kPathLdsBytesPerWave : 0)) *
+    lds += 8 + (rtwk::kHomeLdsBytesPerWave + ((var & rtwk::kVarPathLdsBit) ? rtwk::kPathLdsBytesPerWave : 0) +
+                ((var & rtwk::kVarUnitBaseBit) ? rtwk::kUnitBaseLdsBytesPerWave : 0)) *
                    (rtwk::kTraceBlock / 64);  // (8: alignment of the home block)
   if (lds > 64 * 1024) return fail(RTW_UNSUPPORTED, "scene tables need %zu B of LDS", lds);
   const int bpc = blocks_per_cu(dev, (int)p->precision, lds, var);

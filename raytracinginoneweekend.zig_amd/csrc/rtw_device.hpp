@@ -88,6 +88,13 @@ constexpr int kVarBatchDecode = 1048576;
 // (sampler, scatter, sample start, miss), so neither is held in VGPRs across
 // the closest hit.
 constexpr int kVarPathLds = 33554432;
+// kVarUnitBase (with kVarHomeLds): the unit's RNG block base
+// seed_base + (pixel << 40) * gamma and its f64 pixel column / reference row
+// are made once per unit (home block); a sample's state is then
+// base + s * (gamma << 16) — the same value as (((pixel << 24) | s) << 16) *
+// gamma + seed_base mod 2^64, since s < 2^24 (rtw_validate_params) makes the
+// | an addition — and u, v add the stored f64 coordinates.
+constexpr int kVarUnitBase = 67108864;
 // f64 pretest over spatial clusters of narrow spheres (SceneView ccull...):
 // a wave skips a cluster's member pretests when every lane's line provably
 // misses the cluster's bounding sphere.
@@ -704,6 +711,15 @@ __device__ __forceinline__ void start_sample_uv(const RTW_CONST TraceArgs<R>* Ap
   L.rs = A.seed_base + ((((pixel << 24) | (uint64_t)L.s)) << 16) * kGamma;
   u = rtwm::div_rn((R)L.px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
   v = rtwm::div_rn((R)j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
+}
+// start_sample_uv with the unit's precomputed base and coordinates (kVarUnitBase)
+template <typename R>
+__device__ __forceinline__ void start_sample_uv_base(const RTW_CONST TraceArgs<R>* Ap, Lane<R>& L, uint64_t base,
+                                                     R px, R j, R& u, R& v) {
+  const RTW_CONST TraceArgs<R>& A = *opaque(Ap);
+  L.rs = base + (uint64_t)L.s * (kGamma << 16);
+  u = rtwm::div_rn(px + rnd<R>(L.rs), (R)A.W - (R)1, A.inv_w1);
+  v = rtwm::div_rn(j + rnd<R>(L.rs), (R)A.H - (R)1, A.inv_h1);
 }
 // Part 2, after the lens-disk point (rand.zig:30-36, coop_reject<R, 2>).
 // PRE: the time draw was made by coop_reject_mixed (`traw`, the draw at

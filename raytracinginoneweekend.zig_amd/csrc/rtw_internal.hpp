@@ -130,6 +130,9 @@ constexpr size_t kHomeLdsBytesPerWave = 2560;
 // + (kVarPathLds) the lane's path attenuation T (3 x 8 B) and RNG state (8 B) after it
 constexpr int kVarPathLdsBit = 33554432;
 constexpr size_t kPathLdsBytesPerWave = 4 * 64 * 8;
+// + (kVarUnitBase) the unit's RNG base and f64 pixel column / reference row
+constexpr int kVarUnitBaseBit = 67108864;
+constexpr size_t kUnitBaseLdsBytesPerWave = 3 * 64 * 8;
 #ifndef RTW_DEFAULT_VAR_F32  // (A/B builds override it)
 #define RTW_DEFAULT_VAR_F32 (8 + 512 + 131072 + 262144 + 524288 + 16777216)  // 17695240
 #endif
@@ -194,8 +197,8 @@ struct WfArgs {
   uint32_t batch;      // units per reservoir refill (one atomic on the device queue)
   uint32_t bounces;    // wf_step: bounce segments per path per launch (>= 1), the path kept in registers between them
   uint32_t passes;     // wf_step: queue passes per launch (>= 1): in -> out, out -> in, ... (every segment through the queues)
-  uint32_t* live_acc;  // wf_step (fused): {sum of the launch's final segment counts, workgroups finished}, zero
-                       // between launches (the last workgroup resets them)
+  uint32_t* live_acc;  // wf_step (fused): 8-B aligned 64-bit word, (sum of the launch's final segment counts << 20)
+                       // + workgroups finished; zero between launches (the last workgroup resets it)
   uint32_t* poll_out;  // wf_step (fused): the host's pinned poll word, written by the launch's last workgroup
   uint32_t hit_form;   // 1: queue `in` holds paths WITH their hit (fused engine: hk, and o = the hit point); the drains
                        // then shade the stored hit first instead of tracing the segment again

@@ -73,16 +73,23 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
   double* h_sum = nullptr;    // [3][64]
   uint32_t* h_u32 = nullptr;  // px[64], ly[64], c[64], s_end[64]
   R* h_t = nullptr;           // kVarPathLds: T [3][64] (8-B slots)
+  uint64_t* h_base = nullptr; // kVarUnitBase: the unit's RNG block base [64]
+  R* h_pxj = nullptr;         // kVarUnitBase: its f64 pixel column and reference row [2][64] (8-B slots)
   uint64_t* h_rs = nullptr;   // kVarPathLds: RNG state [64]
   if constexpr (HOME) {
     const size_t off = (size_t)(reinterpret_cast<unsigned char*>(T.cpos + kClusterSlots * S.n_clusters) - lds_raw);
-    constexpr size_t kHomeStride = kHomeLdsBytesPerWave + ((VAR & kVarPathLds) ? kPathLdsBytesPerWave : 0);
+    constexpr size_t kPathB = (VAR & kVarPathLds) ? kPathLdsBytesPerWave : 0;
+    constexpr size_t kHomeStride =
+        kHomeLdsBytesPerWave + kPathB + ((VAR & kVarUnitBase) ? kUnitBaseLdsBytesPerWave : 0);
     unsigned char* hb = lds_raw + ((off + 7) & ~(size_t)7) + (threadIdx.x >> 6) * kHomeStride;
     h_sum = reinterpret_cast<double*>(hb);
     h_u32 = reinterpret_cast<uint32_t*>(hb + 3 * 64 * 8);
     h_t = reinterpret_cast<R*>(hb + 2560);
     h_rs = reinterpret_cast<uint64_t*>(hb + 2560 + 3 * 64 * 8);
+    h_base = reinterpret_cast<uint64_t*>(hb + 2560 + kPathB);
+    h_pxj = reinterpret_cast<R*>(hb + 2560 + kPathB + 64 * 8);
   }
+  constexpr bool UBASE = HOME && (VAR & kVarUnitBase) != 0;
   constexpr bool PLDS = HOME && (VAR & kVarPathLds) != 0 && (VAR & kVarMergedStart) != 0;
   constexpr uint32_t TS = 8 / sizeof(R);  // (8-B slots: T component k of lane l at h_t[(k * 64 + l) * TS])
   auto t_load = [&]() -> V3<R> { return mk(h_t[lid * TS], h_t[(64 + lid) * TS], h_t[(128 + lid) * TS]); };
@@ -175,6 +182,14 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
               h_u32[128 + lid] = c;
               h_u32[192 + lid] = min(L.s + RTW_KA(chunk), RTW_KA(spp));
               h_sum[lid] = h_sum[64 + lid] = h_sum[128 + lid] = z;
+              if constexpr (UBASE) {  // start_sample_uv's per-pixel part, once per unit
+                const uint32_t y = RTW_KA(row_begin) + ly * RTW_KA(row_stride);
+                const uint64_t pixel = (uint64_t)y * RTW_KA(W) + px;
+                h_base[lid] = RTW_KA(seed_base) + (pixel << 40) * kGamma;
+                constexpr uint32_t TS = 8 / sizeof(R);
+                h_pxj[lid * TS] = (R)px;
+                h_pxj[(64 + lid) * TS] = (R)(RTW_KA(H) - 1 - y);
+              }
             } else {
               L.px = px;
               L.ly = ly;
@@ -280,11 +295,15 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       if constexpr (PLDS) L.rs = h_rs[lid];
       R u = (R)0, v = (R)0;
       if (ns) {
-        if constexpr (HOME) {
-          L.px = h_u32[lid];
-          L.ly = h_u32[64 + lid];
+        if constexpr (UBASE) {
+          start_sample_uv_base<R>(kargs<R>(), L, h_base[lid], h_pxj[lid * TS], h_pxj[(64 + lid) * TS], u, v);
+        } else {
+          if constexpr (HOME) {
+            L.px = h_u32[lid];
+            L.ly = h_u32[64 + lid];
+          }
+          start_sample_uv<R>(kargs<R>(), L, u, v);
         }
-        start_sample_uv<R>(kargs<R>(), L, u, v);
       }
       RTW_STAMP(1)
       // dim: 3 unit ball (Lambertian, Metal), 1 the dielectric's draw, 2 lens disk (+ time)

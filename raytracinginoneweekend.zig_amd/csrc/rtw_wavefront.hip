@@ -488,28 +488,32 @@ template <typename R>
 __device__ __forceinline__ const WfArgs<R>& wkargs() {
   return *(const WfArgs<R>*)opaque((const RTW_CONST WfArgs<R>*)__builtin_amdgcn_kernarg_segment_ptr());
 }
-// The host's poll without a kernel of its own (round 6): every wave of a
-// wf_step launch adds its segments' final path counts (lane 0's `sum`) to
-// live_acc[0]; the launch's last workgroup (a ticket in live_acc[1]) writes
-// the total to the host's pinned poll word and zeroes both words for the next
-// launch.  It replaces, per polled batch, a wf_count launch and the copy of
-// its result, which waited in stream order for a CU the other queue set's
-// wf_step held (~50 us each in the kernel trace).  Release / acquire at agent
-// scope order the adds before the ticket; the kernel's end makes the host
-// word visible to the event the host waits on.
+// The host's poll without a kernel of its own (round 6): each workgroup of a
+// wf_step launch sums its waves' final segment path counts (lane 0's `sum`)
+// and adds (sum << 20) + 1 to the 64-bit word live_acc: one relaxed atomic
+// carries both the count and a ticket (low 20 bits; grids stay far below
+// 2^20), so the workgroup that takes the last ticket holds the launch's total
+// in the value its add returns — no fences.  (A first form with agent-scope
+// release / acquire around a separate ticket made the engine 50% slower:
+// every workgroup's fences wrote back and invalidated its XCD's L2 under the
+// waves still running.)  The last workgroup writes the total to the host's
+// pinned poll word and zeroes the accumulator for the next launch; the
+// kernel's end makes the host word visible to the event the host waits on.
+// It replaces, per polled batch, a wf_count launch and the copy of its result.
 template <typename R>
 __device__ __forceinline__ void publish_live(const WfArgs<R>& A, uint32_t sum) {
   if (!A.poll_out) return;  // (wave-uniform: a kernel argument)
-  if ((threadIdx.x & 63u) == 0u && sum) __hip_atomic_fetch_add(A.live_acc, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ uint32_t wg_sum[kTraceBlock / 64];
+  if ((threadIdx.x & 63u) == 0u) wg_sum[threadIdx.x >> 6] = sum;
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t t = __hip_atomic_fetch_add(A.live_acc + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1u == gridDim.x) {
-      const uint32_t total = __hip_atomic_load(A.live_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(A.poll_out, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(A.live_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(A.live_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t g = 0;
+    for (uint32_t w = 0; w < kTraceBlock / 64; ++w) g += wg_sum[w];
+    uint64_t* acc = reinterpret_cast<uint64_t*>(A.live_acc);
+    const uint64_t old = __hip_atomic_fetch_add(acc, (g << 20) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old & 0xFFFFFu) + 1u == gridDim.x) {
+      __hip_atomic_store(A.poll_out, (uint32_t)((old >> 20) + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(acc, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
