@@ -1042,9 +1042,10 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
   if (p->engine != RTW_ENGINE_WAVEFRONT && !rtwk::trace_variant_built((int)p->precision, var))
     return fail(RTW_EINVAL, "RTW_VARIANT=%d: trace kernel variant not built into this library", var);
   // The clustered pretest runs only in the f64 megakernel variants with
-  // kVarCluster, and only when the shutter lies in every time group.
-  const uint32_t cl_on = (p->engine == RTW_ENGINE_MEGAKERNEL && p->precision == RTW_PRECISION_F64 &&
-                          (var & rtwk::kVarClusterBit) != 0)
+  // kVarCluster (or the wavefront kernels built with it: kWfCluster), and only
+  // when the shutter lies in every time group.
+  const uint32_t cl_on = (p->precision == RTW_PRECISION_F64 &&
+                          (p->engine == RTW_ENGINE_MEGAKERNEL ? (var & rtwk::kVarClusterBit) != 0 : rtwk::kWfCluster))
                              ? clusters_usable(sc, cam)
                              : 0u;
   size_t lds = lds_bytes(sc, (int)p->precision, cl_on ? sc->v64.n_clusters : 0u);
@@ -1069,8 +1070,8 @@ int launch_all(rtw_scene sc, const rtw_camera* cam, const rtw_params* p, void* w
     } else {
       rtwk::TraceArgs<double> a;
       fill_args(a, sc->v64, cam, p, ws, L);
-      a.sc.cluster_on = 0u;  // the bounce kernels run the flat pretest
-      a.sc.n_clusters = 0u;
+      a.sc.cluster_on = cl_on;  // (0 unless the bounce kernels were built with the clustered pretest)
+      if (!cl_on) a.sc.n_clusters = 0u;
       st = run_wavefront<double>(a, p, ws, L, dev, lds, stream, mode == 1);
     }
     if (st != RTW_OK) return st;

@@ -123,6 +123,15 @@ int trace_blocks_per_cu(int precision, size_t lds, int var);
 #endif
 constexpr int kDefaultVarF64 = RTW_DEFAULT_VAR_F64;
 constexpr int kVarClusterBit = 2097152;  // rtw_device.hpp kVarCluster (clustered pretest, f64)
+// The wavefront engine's closest-hit variant bits beyond kVarFastSqrt (f64;
+// rtw_wavefront.hip kWfExtendVar): with kVarClusterBit its kernels run the
+// clustered pretest and the host stages the cluster tables for them.  Round 6
+// default: -3.0 % per configs[1] frame (profiles/r06/wf_step_ab.txt; round 2
+// measured it 12 % slower when it spilled in wf_step, which no longer spills).
+#ifndef RTW_WF_VAR_EXTRA  // (A/B builds override it; 0: the flat pretest)
+#define RTW_WF_VAR_EXTRA kVarClusterBit
+#endif
+constexpr bool kWfCluster = (RTW_WF_VAR_EXTRA & kVarClusterBit) != 0;
 // rtw_device.hpp kVarHomeLds: the lane's unit fields and f64 chunk sum in LDS
 // (megakernel), kHomeLdsBytesPerWave per wave after the scene tables.
 constexpr int kVarHomeLdsBit = 16777216;

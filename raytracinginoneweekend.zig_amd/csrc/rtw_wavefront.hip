@@ -140,6 +140,27 @@ __device__ __forceinline__ void start_path(const TraceArgs<R>& A, uint32_t unit,
   start_sample_ray<R>(kargs<R>(), L, u, v, dk[0], dk[1]);
 }
 
+// The same for the lanes with `need` (wave-converged): the lens-disk points
+// from one cooperative pass (coop_reject_mixed, dim 2: the megakernel's
+// merged start) with the sample's time draw made in it, instead of each
+// lane's own rejection loop — the same candidates and states, so the same bits.
+template <typename R>
+__device__ __forceinline__ void start_path_coop(const TraceArgs<R>& A, uint32_t unit, uint32_t s, bool need,
+                                                Lane<R>& L, CoopSlots* slots, uint32_t lid) {
+  R u = (R)0, v = (R)0;
+  if (need) {
+    uint32_t px, ly, c;
+    decode_unit(A, unit, px, ly, c);
+    L.px = px;
+    L.ly = ly;
+    L.s = s;
+    start_sample_uv<R>(kargs<R>(), L, u, v);
+  }
+  R pt[3] = {(R)0, (R)0, (R)0}, raw = (R)0;
+  if (__any(need)) coop_reject_mixed<R>(need ? 2u : 0u, L.rs, pt, raw, slots, lid);
+  if (need) start_sample_ray<R, true>(kargs<R>(), L, u, v, pt[0], pt[1], raw);
+}
+
 // Append the wave's live lanes to its own segment of queue `out` at
 // positions out_n, out_n+1, ... (order kept; no atomics).
 template <typename R>
@@ -219,6 +240,27 @@ __device__ __forceinline__ bool group_has_work(const WfArgs<R>& A) {
 // whether the lane holds a live path afterwards.  STATS: count finished
 // samples and shaded segments (rtw_render_counts); FIN: also as the
 // in-register drain's own counts (stats 9, 10: rtw_render_counts_ex).
+// scatter_hit's variant bits: the megakernel's exact fast f64 sqrt and the
+// host's Schlick r0^2 table (both bit-identical forms); -0.9 % per frame on top
+// of the clustered pretest (profiles/r06/wf_step_ab.txt).
+#ifndef RTW_WF_SCATTER_VAR  // (A/B builds override it; 0: the plain forms)
+#define RTW_WF_SCATTER_VAR (kVarFastSqrt | kVarR0Table)
+#endif
+template <typename R>
+constexpr int kWfScatterVar = RTW_WF_SCATTER_VAR;
+#ifndef RTW_WF_PREDRAW
+#define RTW_WF_PREDRAW 0  // A/B builds: the dielectric's draw inside the bounce's cooperative pass
+#endif
+constexpr bool kWfPreDraw = RTW_WF_PREDRAW != 0;
+#ifndef RTW_WF_COOP_DISK
+#define RTW_WF_COOP_DISK 0  // A/B builds: shade_step's new samples take their lens-disk points cooperatively
+#endif
+constexpr bool kWfCoopDisk = RTW_WF_COOP_DISK != 0;
+#ifndef RTW_WF_LANE_BALL
+#define RTW_WF_LANE_BALL 0  // A/B builds: the bounce's unit-ball points from each lane's own loop
+#endif
+constexpr bool kWfLaneBall = RTW_WF_LANE_BALL != 0;
+
 // The bounce of a lane's path (`valid`) on its closest hit: background on a
 // miss, else Material.scatter; `ended` when the sample is over (miss,
 // absorbed, or the depth bound).  Wave-converged (coop_reject).
@@ -237,12 +279,26 @@ __device__ __forceinline__ void bounce(const WfArgs<R>& A, const LdsTables<R>& T
       shading = true;
     }
   }
-  // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal.
-  const bool nb = shading && kind <= 2u;
-  R b3[3] = {(R)0, (R)0, (R)0};
-  if (__any(nb)) coop_reject<R, 3, true>(nb, L.rs, b3, T.slots, lid);
+  // randomPointInUnitSphere (rand.zig:22-28) for Lambertian and Metal
+  // (kWfPreDraw: and the dielectric's draw, in the same cooperative pass).
+  R b3[3] = {(R)0, (R)0, (R)0}, raw = (R)0;
+  if constexpr (kWfPreDraw) {
+    const uint32_t dim = shading ? (kind <= 2u ? 3u : 1u) : 0u;
+    if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, b3, raw, T.slots, lid);
+  } else if constexpr (kWfLaneBall) {
+    if (shading && kind <= 2u)
+      for (;;) {  // each lane's own rejection loop (rand.zig:22-28)
+        b3[0] = rrange_m11<R>(L.rs);
+        b3[1] = rrange_m11<R>(L.rs);
+        b3[2] = rrange_m11<R>(L.rs);
+        if (in_unit_ball<R, 3>(b3)) break;
+      }
+  } else {
+    const bool nb = shading && kind <= 2u;
+    if (__any(nb)) coop_reject<R, 3, true>(nb, L.rs, b3, T.slots, lid);
+  }
   if (shading) {
-    if (scatter_hit<R, F32, 0, false, true>(T, L, hit, tmax, kind, b3))
+    if (scatter_hit<R, F32, kWfScatterVar<R>, kWfPreDraw, true>(T, L, hit, tmax, kind, b3, raw))
       ended = true;  // absorbed: emitted == 0 (material.zig:31-38)
     else if (L.depth == A.t.max_depth)
       ended = true;  // rayColor(depth == 0) is black (main.zig:105-108)
@@ -301,7 +357,10 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
     hs[0] = hs[1] = hs[2] = z;
     need_sample = true;
   }
-  if (need_sample) start_path(A.t, unit, s, L);
+  if constexpr (kWfCoopDisk)
+    start_path_coop(A.t, unit, s, need_sample, L, T.slots, lid);
+  else if (need_sample)
+    start_path(A.t, unit, s, L);
   if constexpr (STATS) {
     const uint32_t ns = (uint32_t)__popcll(__ballot(ended)), nv = (uint32_t)__popcll(__ballot(valid));
     if (lid == 0) {
@@ -320,10 +379,12 @@ __device__ __forceinline__ bool shade_step(const WfArgs<R>& A, const LdsTables<R
 #define RTW_WF_EXT_OCC 5  // 6 measured 4 % faster per launch but spills 44 B/lane (wf_extend PMC traffic 104 vs 60 GB/frame)
 #endif
 constexpr int kWfExtendOcc = RTW_WF_EXT_OCC;
-// (The clustered pretest, +5 % in the megakernel, made the fused engine 12 % slower:
-// profiles/r02/wf_cluster_ab.txt — its extra registers spill in wf_step.)
+// (The clustered pretest, +5 % in the megakernel, made the fused engine 12 % slower
+// in round 2: profiles/r02/wf_cluster_ab.txt — its extra registers spilled in
+// wf_step.  Without spills since round 6 it is the default: RTW_WF_VAR_EXTRA.)
 template <typename R>
-constexpr int kWfExtendVar = sizeof(R) == 8 ? kVarFastSqrt : 0;
+constexpr int kWfExtendVar = sizeof(R) == 8 ? (kVarFastSqrt | RTW_WF_VAR_EXTRA) : 0;
+
 // ---------------------------------------------------------------- generate --
 // Every slot of the wave's segments takes a unit and starts its first sample.
 // HIT (fused engine): also the first closest hit of every new path.
