@@ -95,6 +95,9 @@ constexpr int kVarPathLds = 33554432;
 // gamma + seed_base mod 2^64, since s < 2^24 (rtw_validate_params) makes the
 // | an addition — and u, v add the stored f64 coordinates.
 constexpr int kVarUnitBase = 67108864;
+// kVarLaneDisk (with kVarMergedStart): new samples' lens-disk points from each
+// lane's own rejection loop after the cooperative pass, not inside it.
+constexpr int kVarLaneDisk = 134217728;
 // f64 pretest over spatial clusters of narrow spheres (SceneView ccull...):
 // a wave skips a cluster's member pretests when every lane's line provably
 // misses the cluster's bounding sphere.

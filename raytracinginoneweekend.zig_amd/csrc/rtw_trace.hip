@@ -308,7 +308,8 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
       RTW_STAMP(1)
       // dim: 3 unit ball (Lambertian, Metal), 1 the dielectric's draw, 2 lens disk (+ time)
       constexpr bool PRE = (VAR & kVarPreDraw) != 0;
-      const uint32_t dim = shading ? (kind <= 2u ? 3u : (PRE ? 1u : 0u)) : (ns ? 2u : 0u);
+      constexpr bool LDISK = (VAR & kVarLaneDisk) != 0;  // new samples' disk points from each lane's own loop
+      const uint32_t dim = shading ? (kind <= 2u ? 3u : (PRE ? 1u : 0u)) : (ns && !LDISK ? 2u : 0u);
       R pt[3] = {(R)0, (R)0, (R)0}, raw = (R)0;
       if (__any(dim != 0u)) coop_reject_mixed<R>(dim, L.rs, pt, raw, slots, lid);
       RTW_STAMP(7)
@@ -317,7 +318,17 @@ __global__ void __launch_bounds__(kTraceBlock, (VAR & 8) ? 5 : ((VAR & 4) ? 4 : 
         if (scatter_hit<R, F32, VAR, PRE>(T, L, hit, tmax, kind, pt, raw)) finish_sample();  // absorbed
       }
       if (ns) {
-        start_sample_ray<R, PRE>(kargs<R>(), L, u, v, pt[0], pt[1], raw);
+        if constexpr (LDISK) {
+          R dk[2];
+          for (;;) {  // randomPointInUnitDisk (rand.zig:30-36)
+            dk[0] = rrange_m11<R>(L.rs);
+            dk[1] = rrange_m11<R>(L.rs);
+            if (in_unit_ball<R, 2>(dk)) break;
+          }
+          start_sample_ray<R>(kargs<R>(), L, u, v, dk[0], dk[1]);
+        } else {
+          start_sample_ray<R, PRE>(kargs<R>(), L, u, v, pt[0], pt[1], raw);
+        }
         have_ray = true;
       }
       if constexpr (PLDS) {
