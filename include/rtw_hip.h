@@ -143,13 +143,13 @@ typedef struct {
 } rtw_params;
 
 #define RTW_DEFAULT_CHUNK 32u
-#define RTW_DEFAULT_WF_PATHS (3u << 18) /* 786,432 in-flight paths (with two sets) */
+#define RTW_DEFAULT_WF_PATHS (5u << 17) /* 655,360 in-flight paths (with two sets; round 6) */
 /* Wavefront queue sets: wf_paths is split over this many independent queue
  * sets, each driven on its own HIP stream (params.wf_sets overrides, 1-4). */
 #define RTW_DEFAULT_WF_SETS 2u
 #define RTW_MAX_WF_SETS 4u
-/* Queue passes per wf_step launch (8 to 16 measured equal, 1 = 19 % slower). */
-#define RTW_DEFAULT_WF_PASSES 8u
+/* Queue passes per wf_step launch (round 6: 16 with the paths above). */
+#define RTW_DEFAULT_WF_PASSES 16u
 #define RTW_MAX_SPHERES 4096u
 
 /* ------------------------------------------------------------ queries -- */

@@ -28,9 +28,9 @@ RTW_OK, RTW_EINVAL, RTW_UNSUPPORTED, RTW_EHIP, RTW_ENOMEM, RTW_ENODEV = 0, -1, -
 LAMBERT_SOLID, LAMBERT_CHECKER, METAL, DIELECTRIC, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 PRECISION = {"f64": 0, "f32": 1}
 ENGINE = {"megakernel": 0, "wavefront": 1}
-DEFAULT_WF_PATHS = 3 << 18  # rtw_hip.h RTW_DEFAULT_WF_PATHS
+DEFAULT_WF_PATHS = 5 << 17  # rtw_hip.h RTW_DEFAULT_WF_PATHS
 DEFAULT_WF_SETS = 2  # rtw_hip.h RTW_DEFAULT_WF_SETS (params.wf_sets overrides)
-DEFAULT_WF_PASSES = 8  # rtw_hip.h RTW_DEFAULT_WF_PASSES (params.wf_passes overrides)
+DEFAULT_WF_PASSES = 16  # rtw_hip.h RTW_DEFAULT_WF_PASSES (params.wf_passes overrides)
 WF_DRAIN = {"samples": 0, "slots": 1, "none": 2}  # rtw_wf_drain
 WF_FORM = {"fused": 0, "split": 1}  # rtw_wf_form
 WORLD_FEATURES = {"auto": 0, "all": 1}  # rtw_world_features

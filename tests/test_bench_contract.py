@@ -83,8 +83,9 @@ def test_wavefront_traffic_is_the_pmc_measurement():
     wf = load("bench.json")["wavefront_variant"]["roofline"]
     t = load("wf_traffic.json", source_round(wf, "wf_traffic.json", "traffic_bytes_per_frame"))
     assert wf["traffic"] == round(t["traffic_bytes_per_frame"])
-    # the queues move close to their algorithmic bytes (no wasted re-reads)
-    assert 0.8 < wf["traffic"] / wf["algorithmic_bytes_per_frame"] < 1.5
+    # the queues move close to their algorithmic bytes (no wasted re-reads; below them since round 6's
+    # smaller queues let the XCDs' L2 serve part of each pass's re-read: 0.77x, profiles/r06/wf_step_ab.txt)
+    assert 0.7 < wf["traffic"] / wf["algorithmic_bytes_per_frame"] < 1.5
     assert abs(wf["frac"] - wf["achieved"] / wf["peak"]) < 1e-3
 
 

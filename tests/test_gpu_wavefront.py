@@ -97,9 +97,9 @@ def test_wavefront_cover_parity(rtw, oracle, cover, precision, w, spp, chunk, pa
     assert_parity(wf[0], o, f"wavefront {precision} {w}x{h}x{spp} chunk {chunk} paths {paths}")
 
 
-@pytest.mark.parametrize("passes", [2, 3, 64])
+@pytest.mark.parametrize("passes", [2, 3, 8, 64])
 def test_wavefront_queue_passes_per_launch(rtw, cover, passes):
-    """params.wf_passes other than the default (8) and 1: an even count
+    """params.wf_passes other than the default (16) and 1: an even count
     returns each launch's output to its input queue, an odd count alternates
     the queues per launch as one pass does; 64 (the maximum) lets a batch run
     past the drain trigger.  Same image as the megakernel."""

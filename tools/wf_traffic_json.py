@@ -10,12 +10,15 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracinginoneweekend.zig_amd"))
+import rtw_amd as R  # noqa: E402  (the library defaults the passes ran with: rtw_hip.h RTW_DEFAULT_WF_*)
+
 fetch_dir, write_dir, out = sys.argv[1], sys.argv[2], sys.argv[3]
 frames = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4].isdigit() else 1
 KERNELS = ("wf_extend", "wf_shade", "wf_step", "wf_finish", "wf_drain")
 FUSED = "--split" not in sys.argv  # the engine form the passes ran (params.wf_form)
-SETS = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--sets=")), 2)  # params.wf_sets
-PASSES = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--passes=")), 8)  # params.wf_passes (fused)
+SETS = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--sets=")), R.DEFAULT_WF_SETS)  # params.wf_sets
+PASSES = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--passes=")), R.DEFAULT_WF_PASSES)  # params.wf_passes
 
 
 def total(d, name):
