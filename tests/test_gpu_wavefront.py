@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from helpers import diff_stats, to_oracle_camera, to_oracle_scene
-from test_gpu_parity import ASPECT, assert_parity, custom_scene, oracle_render
+from test_gpu_parity import ASPECT, assert_parity, clustered_scene, custom_scene, oracle_render
 
 pytestmark = pytest.mark.gpu
 
@@ -136,6 +136,22 @@ def test_wavefront_custom_scene(rtw, oracle, precision):
     assert_identical(mk, wf, f"custom {precision}")
     o = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam), **kw)
     assert_parity(wf[0], o, f"wavefront custom {precision}")
+
+
+@pytest.mark.parametrize("time1", [1.0, 1.2])
+def test_wavefront_clustered_pretest(rtw, oracle, time1):
+    """The bounce kernels run the megakernel's clustered pretest since round 6
+    (rtw_internal.hpp RTW_WF_VAR_EXTRA): three time groups mixed in clusters,
+    odd cluster sizes, with a shutter inside every group (clusters on) and one
+    outside a group (clusters off, the flat pretest) — the megakernel's image
+    bit for bit and the oracle's."""
+    sph, mats = clustered_scene(rtw)
+    cam = rtw.camera_init((13, 2, 3), (0, 0.3, 0), (0, 1, 0), 30.0, ASPECT, 0.1, 10.0, 0.0, time1)
+    kw = dict(width=192, height=108, spp=12, chunk=5)
+    mk, wf = both(rtw, cam, sph, mats, wf_paths=4096, **kw)
+    assert_identical(mk, wf, f"clustered scene, shutter [0, {time1}]")
+    o = oracle_render(oracle, to_oracle_scene(oracle, sph, mats), to_oracle_camera(oracle, cam), **kw)
+    assert_parity(wf[0], o, f"wavefront clustered scene, shutter [0, {time1}]")
 
 
 def test_wavefront_row_shards(rtw, cover):
