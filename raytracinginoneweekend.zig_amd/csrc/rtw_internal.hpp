@@ -271,6 +271,27 @@ constexpr uint32_t kBvhStack = 32;  // per-wave LDS stack entries (the builder c
 // a BVH of depth <= kLaneStack never overflows it (a push per level at most);
 // deeper BVHs take the union walk
 constexpr uint32_t kLaneStack = 16;
+// ... of which kLaneStack - 1 in LDS rows: the walk keeps the stack's top entry
+// in a register, and a tree of depth D holds at most D pending nodes (one
+// sibling per level of the current path: pops take the deepest), so D - 1 rows
+// (RTW_LANE_STACK_LDS: the rows built; the default keeps kLaneStack, one to spare)
+#ifndef RTW_LANE_STACK_LDS
+#define RTW_LANE_STACK_LDS kLaneStack
+#endif
+constexpr uint32_t kLaneStackLds = RTW_LANE_STACK_LDS;
+static_assert(kLaneStackLds + 1 >= kLaneStack, "a depth-kLaneStack tree must fit the LDS rows + the top register");
+// The per-lane walk's node cache: the first kNodeCache node records (the top
+// of the tree in breadth-first order, rtw_world_capi.hip top_first) staged in
+// LDS once per workgroup; a lane visiting one reads it with ds_read instead of
+// three vector loads through the TA/TD pipe that bounds the walk.  0: none —
+// the default: 21 records (with RTW_LANE_STACK_LDS 15 to fit four workgroups
+// per CU) measured equal on the globe, 31.67 vs 31.29 ms (the walk pays per
+// wave iteration, ~41 per segment for ~18 visits per lane, not per lane-load);
+// profiles/r06/world_ncache_ab.txt.
+#ifndef RTW_NODE_CACHE
+#define RTW_NODE_CACHE 0
+#endif
+constexpr uint32_t kNodeCache = RTW_NODE_CACHE;
 // per-lane walk: a paused walk keeps its closest hit's stored position + 1 in
 // the low kTravPosBits of one LDS word (rtw_world.hip LaneTravRows)
 constexpr uint32_t kTravPosBits = 26;

@@ -512,9 +512,11 @@ struct LaneTravRows {                     // one wave's rows, [field][lane]
 // columns, the LaneTrav rows and the attenuation rows (3 f64 per lane).  With
 // the static tail rows (5 words per lane) and chunk sums (3 f64) a 4-wave
 // workgroup holds 40 KB: four fit the CU's 160 KB (4 waves per SIMD).
-constexpr uint32_t kLaneWaveWords = (kLaneStack + kTravWords + 6u) * 64u;
-static_assert((kLaneWaveWords + (5u + 6u) * 64u) * 4u * (kWorldBlock / 64) * 4u <= 160u * 1024u,
+constexpr uint32_t kLaneWaveWords = (kLaneStackLds + kTravWords + 6u) * 64u;
+// (+ the node cache: 48 B per cached node record, once per workgroup)
+static_assert(((kLaneWaveWords + (5u + 6u) * 64u) * 4u * (kWorldBlock / 64) + kNodeCache * 48u) * 4u <= 160u * 1024u,
               "per-lane kernel: four 4-wave workgroups per CU");
+typedef float nf4 __attribute__((ext_vector_type(4)));
 // Starts a walk from the root for this lane (no hit yet).
 __device__ __forceinline__ void trav_begin(LaneTravRows* R, uint32_t lid) {
   R->w[0][lid] = 0u;  // the root node
@@ -529,7 +531,8 @@ __device__ __forceinline__ void trav_begin(LaneTravRows* R, uint32_t lid) {
 // One traversal phase of the lanes with `walking` set; returns true for the
 // lanes whose walk finished in it (`h` = the closest hit).  Wave-converged.
 template <int MODE, int FEAT, typename WV>
-__device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, LaneTravRows* R, uint32_t lid,
+__device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, LaneTravRows* R, const nf4* ncache,
+                                           uint32_t lid,
                                            bool walking, uint32_t yield_lanes, const V& o, const V& d, D time, D tmin,
                                            WHit& h, unsigned long long& nv, unsigned long long& nt,
                                            unsigned long long& wi, unsigned long long& wl) {
@@ -609,10 +612,15 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
       if (step) {
         if (MODE == 1) ++nv;
         // (a 32-bit byte offset from the SGPR base: the loads' saddr form, no 64-bit address math)
-        typedef float f4 __attribute__((ext_vector_type(4)));
+        typedef nf4 f4;
         const __attribute__((address_space(1))) f4* nd = reinterpret_cast<const __attribute__((address_space(1))) f4*>(
             reinterpret_cast<const __attribute__((address_space(1))) char*>(nodes) + (ref << 6));
-        const f4 q0 = nd[0], q1 = nd[1], q2 = nd[2];
+        f4 q0, q1, q2;
+        if (PACKED && kNodeCache > 0 && ref < kNodeCache) {  // the top of the tree: the workgroup's LDS copy
+          q0 = ncache[3u * ref], q1 = ncache[3u * ref + 1u], q2 = ncache[3u * ref + 2u];
+        } else {
+          q0 = nd[0], q1 = nd[1], q2 = nd[2];
+        }
         // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3 (refs in words 12-13);
         // the per-lane constants two to a register pair (pk_fma_sel)
         const f2 x0 = pk_fma_sel<0, 0>(f2{q0.x, q0.y}, I1, O1), x1 = pk_fma_sel<0, 1>(f2{q1.z, q1.w}, I1, O2);
@@ -766,8 +774,11 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
                     (threadIdx.x >> 6) * ((FEAT & kFeatLane) ? kLaneWaveWords : kBvhStack);
   // per-lane traversal: this wave's LaneTrav rows follow its stack columns,
   // and the lanes' attenuation rows (T) follow them
-  LaneTravRows* trav_rows = reinterpret_cast<LaneTravRows*>(stack + kLaneStack * 64u);
-  double(*t_rows)[64] = reinterpret_cast<double(*)[64]>(stack + (kLaneStack + kTravWords) * 64u);
+  LaneTravRows* trav_rows = reinterpret_cast<LaneTravRows*>(stack + kLaneStackLds * 64u);
+  double(*t_rows)[64] = reinterpret_cast<double(*)[64]>(stack + (kLaneStackLds + kTravWords) * 64u);
+  // the per-lane walk's node cache (packed refs): the top kNodeCache records, words 0-11
+  constexpr bool NCACHE = (FEAT & kFeatLane) != 0 && (FEAT & kFeatPacked) != 0 && kNodeCache > 0;
+  const nf4* node_cache = nullptr;  // (staged below; no LDS at all when NCACHE is off)
   // Tail dealing rows of this wave's lanes (lane = the owner of a unit): the
   // first sample handed to other lanes (samples [hi, s_end) are theirs), the
   // ring entries they filled, the unit's pixel; and the dealing list.
@@ -800,6 +811,14 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
 #define WKA(f) (opaque((const RTW_CONST WorldArgs*)__builtin_amdgcn_kernarg_segment_ptr())->f)
   const uint32_t* order = W.order;
   const uint32_t lid = lane_id();
+  if constexpr (NCACHE) {  // stage the node cache (every thread reaches this before the persistent loop)
+    __shared__ nf4 ncache_lds[(kNodeCache > 0 ? kNodeCache : 1u) * 3u];
+    const uint32_t nn = min(W.n_nodes, kNodeCache);
+    const nf4* gn = reinterpret_cast<const nf4*>(W.node);
+    for (uint32_t i = threadIdx.x; i < 3u * nn; i += kWorldBlock) ncache_lds[i] = gn[(i / 3u) * 4u + i % 3u];
+    __syncthreads();
+    node_cache = ncache_lds;
+  }
   Lane<D> L;
   L.px = L.ly = L.c = L.s = L.s_end = L.depth = 0;
   L.rs = 0;
@@ -1092,7 +1111,7 @@ __global__ void __launch_bounds__(kWorldBlock, OCC) world_kernel(WorldArgs A) {
       // holds its unit: ADVICE r5 — and is gone.)
       const uint32_t yl = WKA(lane_yield);
       WHit h;
-      if (trav_phase<MODE, FEAT>(W, WKA(margin), stack, trav_rows, lid, walking, yl, L.o, L.d, L.time, WKA(t.tmin),
+      if (trav_phase<MODE, FEAT>(W, WKA(margin), stack, trav_rows, node_cache, lid, walking, yl, L.o, L.d, L.time, WKA(t.tmin),
                                  h, n_visits, n_tests, n_wi, n_wl)) {
         walking = false;
         shade(h);

@@ -129,6 +129,41 @@ float lower_with_low8(float f, uint32_t payload) {  // the largest float <= f wh
   std::memcpy(&f, &c, 4);
   return f;
 }
+// The per-lane walk's node cache (rtw_world.hip, kNodeCache records in LDS)
+// holds the first records: renumber so that the top of the tree comes first,
+// breadth-first from the root; the other records keep their depth-first order
+// (child 0 of an interior node is still its next record below the top).  Only
+// the layout changes: every traversal follows refs, so no result can.
+void top_first(Bvh& b, uint32_t k) {
+  if (b.n_nodes <= 1 || k <= 1) return;
+  std::vector<uint32_t> first{0u};
+  for (size_t i = 0; i < first.size() && first.size() < k; ++i)
+    for (int c = 0; c < 2 && first.size() < k; ++c) {
+      uint32_t ref;
+      std::memcpy(&ref, b.nodes.data() + (size_t)rtwk::kNodeWords * first[i] + 12 + c, 4);
+      if (!(ref & rtwk::kLeafBit)) first.push_back(ref);
+    }
+  std::vector<uint32_t> id(b.n_nodes, ~0u);
+  for (uint32_t i = 0; i < first.size(); ++i) id[first[i]] = i;
+  uint32_t next = (uint32_t)first.size();
+  for (uint32_t n = 0; n < b.n_nodes; ++n)
+    if (id[n] == ~0u) id[n] = next++;
+  std::vector<float> out(b.nodes.size(), 0.0f);  // (the same size: the padding record after the last stays)
+  for (uint32_t n = 0; n < b.n_nodes; ++n) {
+    float* d = out.data() + (size_t)rtwk::kNodeWords * id[n];
+    std::memcpy(d, b.nodes.data() + (size_t)rtwk::kNodeWords * n, rtwk::kNodeWords * 4);
+    for (int c = 0; c < 2; ++c) {
+      uint32_t ref;
+      std::memcpy(&ref, d + 12 + c, 4);
+      if (!(ref & rtwk::kLeafBit)) {
+        ref = id[ref];
+        std::memcpy(d + 12 + c, &ref, 4);
+      }
+    }
+  }
+  b.nodes.swap(out);
+}
+
 bool pack_refs(Bvh& b, uint32_t n_prims, bool debug) {
   if (b.n_nodes >= 0x800000u || n_prims >= 0x400000u || b.max_leaf > 2u) return false;
   std::vector<float> packed(b.nodes);
@@ -428,6 +463,8 @@ int rtw_world_create(const rtw_world_desc* d, uint32_t flags, rtw_world* out) {
                 nd[0 + c], nd[6 + c], nd[2 + c], nd[8 + c], nd[4 + c], nd[10 + c]);
       }
     }
+    // (leaf-of-one trees are the per-lane walk's: its node cache wants the top first)
+    if (bvh.max_leaf == 1) top_first(bvh, rtwk::kNodeCache);
     (void)pack_refs(bvh, d->n_prims, (flags & RTW_WORLD_DEBUG_BVH) != 0);  // (after the diagnostic: it prints the boxes as built)
   } else {
     for (uint32_t i = 0; i < d->n_prims; ++i) bvh.order.push_back(i);
