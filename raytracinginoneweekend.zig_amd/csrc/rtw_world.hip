@@ -621,6 +621,9 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
         } else {
           q0 = nd[0], q1 = nd[1], q2 = nd[2];
         }
+#if RTW_LANE_TOUCH  // A/B builds: also touch record ref + 1 (child 0 when interior: depth-first layout)
+        const float touch = nd[4].x;
+#endif
         // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3 (refs in words 12-13);
         // the per-lane constants two to a register pair (pk_fma_sel)
         const f2 x0 = pk_fma_sel<0, 0>(f2{q0.x, q0.y}, I1, O1), x1 = pk_fma_sel<0, 1>(f2{q1.z, q1.w}, I1, O2);
@@ -655,6 +658,9 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
           nx = first0 ? r0 : r1;
         }
         ref = nx != kNoRef ? nx : pop();
+#if RTW_LANE_TOUCH
+        asm volatile("" ::"v"(touch));  // (its wait here, at the end of the step)
+#endif
         if (ref != kNoRef && ref >= LB && pend == kNoRef) {  // postpone the leaf, keep walking
           pend = ref;
           ref = pop();
