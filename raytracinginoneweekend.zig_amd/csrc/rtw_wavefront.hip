@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(kTraceBlock) wf_shade(WfArgs<R> A) {
 // the closest hit of the lane's next ray (the bounced ray or the next
 // sample's camera ray) in registers; live paths are appended to the output
 // queue WITH their hit, so no separate extend launch re-reads the rays.
-// Per bounce segment: path + hit read (108 B f64), path + hit written.
+// Per bounce segment: path + hit read (100 B f64: the hit point in o, no root), path + hit written.
 #ifndef RTW_WF_STEP_OCC
 #define RTW_WF_STEP_OCC 5  // profiles/r02/wf_step_ab.txt: 5 waves (32-B spill) ~3 % faster than 4
 #endif
