@@ -209,3 +209,22 @@ def test_no_cpu_fallback_without_gpu(rtw):
     with pytest.raises(rtw.RtwError) as e:
         rtw.render(rtw.cover_camera(16 / 9), sph, mats, rtw.make_params(16, 9, 1))
     assert e.value.status == rtw.RTW_ENODEV
+
+
+def test_python_engine_defaults_are_the_headers(rtw):
+    """rtw_amd's DEFAULT_WF_* / DEFAULT_CHUNK (what bench.py reports and
+    matches PMC evidence against) are the C header's RTW_DEFAULT_* values, so a
+    default changed on one side only cannot label a line with the wrong
+    configuration (round 6 changed the wavefront's paths and passes)."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "rtw_hip.h")).read()
+
+    def define(name):
+        m = re.search(rf"#define {name} \(?(\d+)u(?: << (\d+))?\)?", hdr)
+        assert m, name
+        return int(m.group(1)) << int(m.group(2) or 0)
+
+    assert rtw.DEFAULT_WF_PATHS == define("RTW_DEFAULT_WF_PATHS")
+    assert rtw.DEFAULT_WF_SETS == define("RTW_DEFAULT_WF_SETS")
+    assert rtw.DEFAULT_WF_PASSES == define("RTW_DEFAULT_WF_PASSES")
+    assert rtw.DEFAULT_CHUNK == define("RTW_DEFAULT_CHUNK")
