@@ -86,17 +86,19 @@ constexpr int kVarBatchDecode = 1048576;
 // kVarPathLds (with kVarHomeLds and kVarMergedStart): the lane's attenuation T and
 // RNG state live in its LDS home block between the phases that use them
 // (sampler, scatter, sample start, miss), so neither is held in VGPRs across
-// the closest hit.
+// the closest hit (measurement: within noise).
 constexpr int kVarPathLds = 33554432;
 // kVarUnitBase (with kVarHomeLds): the unit's RNG block base
 // seed_base + (pixel << 40) * gamma and its f64 pixel column / reference row
 // are made once per unit (home block); a sample's state is then
 // base + s * (gamma << 16) — the same value as (((pixel << 24) | s) << 16) *
 // gamma + seed_base mod 2^64, since s < 2^24 (rtw_validate_params) makes the
-// | an addition — and u, v add the stored f64 coordinates.
+// | an addition — and u, v add the stored f64 coordinates (measurement:
+// within noise).
 constexpr int kVarUnitBase = 67108864;
 // kVarLaneDisk (with kVarMergedStart): new samples' lens-disk points from each
-// lane's own rejection loop after the cooperative pass, not inside it.
+// lane's own rejection loop after the cooperative pass, not inside it
+// (measurement: 4.8 % slower, profiles/r06/mk_var_ab.txt).
 constexpr int kVarLaneDisk = 134217728;
 // f64 pretest over spatial clusters of narrow spheres (SceneView ccull...):
 // a wave skips a cluster's member pretests when every lane's line provably

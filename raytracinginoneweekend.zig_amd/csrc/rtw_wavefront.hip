@@ -249,15 +249,18 @@ __device__ __forceinline__ bool group_has_work(const WfArgs<R>& A) {
 template <typename R>
 constexpr int kWfScatterVar = RTW_WF_SCATTER_VAR;
 #ifndef RTW_WF_PREDRAW
-#define RTW_WF_PREDRAW 0  // A/B builds: the dielectric's draw inside the bounce's cooperative pass
+#define RTW_WF_PREDRAW 0  // A/B builds: the dielectric's draw inside the bounce's cooperative pass (neutral;
+                          // profiles/r06/wf_step_ab.txt item 6)
 #endif
 constexpr bool kWfPreDraw = RTW_WF_PREDRAW != 0;
 #ifndef RTW_WF_COOP_DISK
 #define RTW_WF_COOP_DISK 0  // A/B builds: shade_step's new samples take their lens-disk points cooperatively
+                            // (2.5 % slower; wf_step_ab.txt item 6)
 #endif
 constexpr bool kWfCoopDisk = RTW_WF_COOP_DISK != 0;
 #ifndef RTW_WF_LANE_BALL
-#define RTW_WF_LANE_BALL 0  // A/B builds: the bounce's unit-ball points from each lane's own loop
+#define RTW_WF_LANE_BALL 0  // A/B builds: the bounce's unit-ball points from each lane's own loop (1.0 %
+                            // slower; wf_step_ab.txt item 7)
 #endif
 constexpr bool kWfLaneBall = RTW_WF_LANE_BALL != 0;
 

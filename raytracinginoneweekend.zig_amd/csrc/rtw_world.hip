@@ -621,7 +621,8 @@ __device__ __forceinline__ bool trav_phase(const WV& W, D m, uint32_t* lstack, L
         } else {
           q0 = nd[0], q1 = nd[1], q2 = nd[2];
         }
-#if RTW_LANE_TOUCH  // A/B builds: also touch record ref + 1 (child 0 when interior: depth-first layout)
+#if RTW_LANE_TOUCH  // A/B builds: also touch record ref + 1 (child 0 when interior: depth-first layout;
+                    // 5.8 % slower on the globe, profiles/r06/world_touch_ab.txt)
         const float touch = nd[4].x;
 #endif
         // {child 0, child 1} per axis: words {lo0, lo1} x3 then {hi0, hi1} x3 (refs in words 12-13);
