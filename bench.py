@@ -760,7 +760,7 @@ def main():
             "note": "megakernel is VALU-issue bound (valu_issue.busy_frac: the fraction of SIMD cycles in "
                     "which the VALU issues; f64, f32 and integer-multiply wave64 instructions each take ~4 cycles) plus "
                     "divergence; `achieved` counts only the algorithm's sphere-test flops; MFMA n/a (no "
-                    "contraction); HBM traffic is ~24 B per 32 samples by construction (DESIGN.md §Roofline)",
+                    "contraction); HBM traffic is ~24 B per chunk of samples by construction (DESIGN.md §Roofline)",
         }
     else:  # wavefront headline: HBM-bound path queues
         byts = wf_frame_bytes(args, rend.counts(cam, params), rc * W * n_chunks)

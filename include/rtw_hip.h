@@ -142,7 +142,12 @@ typedef struct {
                                  in the place of v4's `reserved`: same layout, and 0 keeps the default.) */
 } rtw_params;
 
-#define RTW_DEFAULT_CHUNK 32u
+/* Samples per accumulation chunk (a work unit = one pixel x one chunk; the
+ * image's per-pixel sum adds each chunk's samples in order, then the chunks in
+ * order: DESIGN.md §2).  Round 6: 20 (was 32) — every engine equal or faster,
+ * the world kernel 3-10 % (profiles/r06/chunk_ab.txt); 20 divides every
+ * configured spp (100, 200, 500, 2000). */
+#define RTW_DEFAULT_CHUNK 20u
 #define RTW_DEFAULT_WF_PATHS (5u << 17) /* 655,360 in-flight paths (with two sets; round 6) */
 /* Wavefront queue sets: wf_paths is split over this many independent queue
  * sets, each driven on its own HIP stream (params.wf_sets overrides, 1-4). */

@@ -41,9 +41,9 @@ extern "C" {
 enum { RO_LAMBERT_SOLID = 0, RO_LAMBERT_CHECKER = 1, RO_METAL = 2, RO_DIELECTRIC = 3 };
 
 /* Chunk of the GPU contract's per-pixel sum when params.chunk == 0 (rtw_hip.h
- * RTW_DEFAULT_CHUNK): chunks of 32 samples summed in order; spp <= 32 is the
+ * RTW_DEFAULT_CHUNK): chunks of 20 samples summed in order; spp <= 20 is the
  * reference's own sequential sum (main.zig:388-393). */
-#define RO_DEFAULT_CHUNK 32u
+#define RO_DEFAULT_CHUNK 20u
 
 typedef struct {
   double c0[3];     /* Sphere.center / MovingSphere.center0 */

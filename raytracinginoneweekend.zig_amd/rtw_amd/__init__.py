@@ -39,7 +39,7 @@ STATS_WORDS = 16  # rtw_hip.h RTW_STATS_WORDS
 STAT_NAMES = ["samples", "segments", "f32_skips", "cand_wave_iters", "cand_lanes", "disc_ge0_lanes",
               "sphere_loop_wave_iters", "cull_survivor_lanes", "cull_exact_wave_iters", "drain_segments",
               "drain_samples", "cluster_wave_tests", "cluster_wave_skips", "drain_wave_iters"]  # RTW_STAT_*
-DEFAULT_CHUNK = 32
+DEFAULT_CHUNK = 20
 COVER_BACKGROUND = (0.70, 0.80, 1.00)
 
 

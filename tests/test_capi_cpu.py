@@ -104,7 +104,7 @@ def test_scene_rejects_bad_material_index(rtw):
 def test_workspace_bytes(rtw):
     p = rtw.make_params(1200, 675, 500)
     n = rtw.workspace_bytes(p)
-    chunks = (500 + 31) // 32
+    chunks = -(-500 // rtw.DEFAULT_CHUNK)  # (rtw_hip.h RTW_DEFAULT_CHUNK)
     assert n >= chunks * 1200 * 675 * 3 * 8
     assert n < chunks * 1200 * 675 * 3 * 8 + 4096
 

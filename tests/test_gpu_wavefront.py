@@ -188,8 +188,9 @@ def test_wavefront_config2_full_frame_identical(rtw, cover, precision, bounces):
     assert_identical(outs[0], outs[1], f"config2 {precision}")
 
 
-@pytest.mark.parametrize("w,spp,paths", [(400, 128, 360_000), (1200, 64, 0), (160, 40, 64), (160, 40, 256)])
-def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, drain, queue_sets):
+@pytest.mark.parametrize("w,spp,paths,chunk", [(400, 128, 360_000, 0), (1200, 64, 0, 0), (160, 40, 64, 0),
+                                               (160, 40, 256, 32)])
+def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, chunk, drain, queue_sets):
     """Statistics pass: the wavefront shades exactly W*H*spp samples and the
     megakernel's number of bounce segments.  Duplicated or lost units would
     leave the image bits unchanged (a unit's samples are deterministic) but
@@ -201,8 +202,8 @@ def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, d
     sph, mats, cam, _, _ = cover
     h = rtw.image_height(w, ASPECT)
     R = TorchRenderer(sph, mats, 0)
-    mk = R.counts(cam, rtw.make_params(w, h, spp))
-    wf = R.counts(cam, rtw.make_params(w, h, spp, engine="wavefront", wf_paths=paths))
+    mk = R.counts(cam, rtw.make_params(w, h, spp, chunk=chunk))
+    wf = R.counts(cam, rtw.make_params(w, h, spp, chunk=chunk, engine="wavefront", wf_paths=paths))
     torch.cuda.synchronize()
     assert mk["samples"] == w * h * spp
     assert (wf["samples"], wf["segments"]) == (mk["samples"], mk["segments"])
@@ -215,6 +216,8 @@ def test_wavefront_traces_every_sample_exactly_once(rtw, cover, w, spp, paths, d
         # (one 64-path segment on the sky units the queue deals last: every
         # slot's last unit ends in the same bounce, so no poll sees slots
         # retiring and the drain may not run at all; 256 paths, split over
-        # at most 2 sets, is the small case whose drain must run)
+        # at most 2 sets, is the small case whose drain must run — with units
+        # of 32 samples: the default 20's shorter units can all end inside one
+        # polled batch of 32 bounces, so that no poll sees slots retiring)
         if (paths or rtw.DEFAULT_WF_PATHS) // queue_sets > 64:
             assert wf["drain_segments"] > 0 and wf["drain_samples"] > 0

@@ -3,7 +3,7 @@ N renders, HIP events around the bounce loop.
   python tools/wf_bench.py [N] [CFG ...]
 CFG (in-process A/B, configurations interleaved per round): comma-separated
 rtw_params fields "paths=<wf_paths>", "sets=<wf_sets>", "drain=samples|slots|none",
-"form=fused|split", "bounces=<wf_bounces>", "passes=<wf_passes>", and environment settings that only a -DRTW_MEASURE library
+"form=fused|split", "bounces=<wf_bounces>", "passes=<wf_passes>", "chunk=<chunk>", and environment settings that only a -DRTW_MEASURE library
 reads (development knobs, e.g. "RTW_WF_GRID=4"); "-" is the default configuration."""
 import os
 import sys
@@ -42,6 +42,8 @@ def apply(cfg):
             kw["wf_bounces"] = int(v)
         elif k == "passes":
             kw["wf_passes"] = int(v)
+        elif k == "chunk":
+            kw["chunk"] = int(v)
         else:
             os.environ[k] = v
     return R.make_params(W, H, spp, engine="wavefront", **kw)
